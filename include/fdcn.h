@@ -1,0 +1,154 @@
+/*
+ * fdcn.h -- C ABI of the MI355X Crank-Nicolson finite-difference engine.
+ *
+ * TEST/PRODUCT BOUNDARY.  This header is the drop-in seam for the reference's
+ * time-stepping hot path.  The reference (rwx-gigaba-sonwabo/Finite_Difference)
+ * is pure Python and has no FFI; its seam is a pair of Python methods, which
+ * the entry points below replace one-for-one:
+ *
+ *   fdcn_cn_batch  <- DiscreteBarrierFDMPricer._solve_grid
+ *                       (discrete_barrier_fdm_pricer.py:442-547)
+ *                     DiscreteBarrierCrankNicolsonLog._solve_grid
+ *                       (discrete_barrier_fdm_pricer_cn.py:219-302)
+ *                     KO projection _apply_KO_projection (…pricer.py:413-440,
+ *                       …_cn.py:199-213) is fused in.
+ *   fdcn_it_batch  <- AmericanFDMPricer._solve_segment
+ *                       (fd_american_equity.py:559-726), Ikonen-Toivanen.
+ *
+ * The Python side (finite_difference_amd/capi.py) binds them with ctypes; the
+ * binding a maintainer would add to the reference is in INTEGRATION.md.
+ *
+ * Conventions
+ *   - A launch solves B independent scenarios ("solves") that share n_nodes,
+ *     n_time and n_ranna.  Everything else is per scenario.
+ *   - n_nodes counts ALL grid nodes including the two Dirichlet nodes:
+ *     node 0 (S_min side), node n_nodes-1 (S_max side), interior 1..n_nodes-2.
+ *     The production barrier engine's top-node drop (…pricer.py:449,543) is
+ *     expressed by the caller passing n_nodes = N_s and v_init = payoff[0:N_s];
+ *     the kernel has no quirk flag.
+ *   - Step m = 0..n_time-1 advances tau to tau_m = tau0 + (m+1)*dt and uses
+ *     theta = 1 for m < n_ranna (Rannacher), 0.5 afterwards.
+ *   - All arrays are C-contiguous, row-major, fp64 / int32.  The caller owns
+ *     every buffer; nothing is retained after return.
+ *   - Return 0 on success, a negative FDCN_E* code on failure; the message is
+ *     available from fdcn_last_error() (thread-local).  Never aborts.
+ */
+#ifndef FDCN_H
+#define FDCN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FDCN_ABI_VERSION 1
+
+/* ---- per-scenario fp64 parameters: params[b*FDCN_NPARAM + k] ---------- */
+enum fdcn_param {
+  FDCN_P_DT = 0,  /* time step (years)                                       */
+  FDCN_P_A,       /* operator coefficient of V_{j-1}: alpha - beta_adv       */
+  FDCN_P_C,       /* operator coefficient of V_{j+1}: alpha + beta_adv       */
+  FDCN_P_BC,      /* operator coefficient of V_j:     -2*alpha - r           */
+  FDCN_P_TAU0,    /* tau at the start of this segment                        */
+  FDCN_P_LO_C0,   /* lower Dirichlet value, see FDCN_I_LO_FORM               */
+  FDCN_P_LO_E0,
+  FDCN_P_LO_C1,
+  FDCN_P_LO_E1,
+  FDCN_P_HI_C0,   /* upper Dirichlet value, see FDCN_I_HI_FORM               */
+  FDCN_P_HI_E0,
+  FDCN_P_HI_C1,
+  FDCN_P_HI_E1,
+  FDCN_NPARAM
+};
+
+/* ---- per-scenario int32 parameters: iparams[b*FDCN_NIPARAM + k] ------- */
+enum fdcn_iparam {
+  FDCN_I_LO_FORM = 0, /* 0: c0*exp(e0*tau) + c1*exp(e1*tau)
+                         1: ((c0*exp(e0*tau))*c1)*exp(e1*tau)  (…pricer.py:391) */
+  FDCN_I_HI_FORM,
+  FDCN_I_KO_LO,       /* monitor steps set V_j = rebate for j <= KO_LO (-1: none) */
+  FDCN_I_KO_HI,       /* … and for j >= KO_HI (>= n_nodes: none)                 */
+  FDCN_I_MON_START,   /* offset of this scenario's entries in mon_step/mon_rebate */
+  FDCN_I_MON_COUNT,   /* number of entries (sorted ascending, values in 1..n_time) */
+  FDCN_I_TAU_MODE,    /* 0: tau0+(m+1)*dt.  1: tau accumulated by repeated +dt as
+                         fd_american_equity.py:664-724 does.  The GPU engine always
+                         uses form 0 (ulp-level difference). */
+  FDCN_NIPARAM
+};
+
+/* error codes */
+#define FDCN_OK 0
+#define FDCN_EINVAL (-1)   /* bad argument / unsupported size                  */
+#define FDCN_EHIP (-2)     /* HIP runtime error                                */
+#define FDCN_ENODEV (-3)   /* no usable gfx950 device                          */
+#define FDCN_ENOMEM (-4)   /* device allocation failed                         */
+
+/* ---- host-pointer entry points (copy in, solve, copy out) ------------- */
+
+/* European solve with knock-out projection on monitor steps.
+ *   v_init     [B][n_nodes]  value vector at tau0 (payoff for a full solve)
+ *   mon_step   [n_mon]       step numbers m+1 at which to project (per scenario
+ *                            a sorted run addressed by MON_START/MON_COUNT)
+ *   mon_rebate [n_mon]       value written into knocked-out nodes at that step
+ *   v_out      [B][n_nodes]  value vector at tau0 + n_time*dt
+ */
+int fdcn_cn_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                  const double* params, const int32_t* iparams,
+                  const double* v_init,
+                  int32_t n_mon, const int32_t* mon_step, const double* mon_rebate,
+                  double* v_out);
+
+/* American solve with Ikonen-Toivanen early exercise against payoff.
+ *   payoff [B][n_nodes]  exercise value phi_j (only interior nodes are used);
+ *   lambda starts at 0 in every call, as _solve_segment does (…equity.py:661).
+ *   KO fields of iparams must be -1 / >= n_nodes and MON_COUNT 0.
+ */
+int fdcn_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                  const double* params, const int32_t* iparams,
+                  const double* v_init, const double* payoff,
+                  double* v_out);
+
+/* ---- device-pointer entry points (all pointers are device memory) ----- */
+/* `stream` is a hipStream_t (NULL = default stream); the call is
+ * asynchronous on that stream and performs no allocation or host sync, so
+ * it may be captured into a hipGraph.  Inputs and output may alias
+ * (v_out == v_init) only if `v_init` is not needed afterwards.
+ * `k_cap` bounds the boundary-layer correction table (see fdcn_sm_extent);
+ * pass the value fdcn_sm_extent returns for the same params.  A scenario whose
+ * extent exceeds k_cap gets NaN outputs (loud, never silently wrong). */
+int fdcn_cn_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                      const double* params, const int32_t* iparams,
+                      const double* v_init,
+                      int32_t n_mon, const int32_t* mon_step, const double* mon_rebate,
+                      double* v_out, int32_t k_cap, void* stream);
+
+int fdcn_it_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                      const double* params, const int32_t* iparams,
+                      const double* v_init, const double* payoff,
+                      double* v_out, int32_t k_cap, void* stream);
+
+/* ---- launch planning / introspection ---------------------------------- */
+/* Writes the kernel geometry chosen for a launch: waves per scenario,
+ * nodes per lane, scenarios per workgroup, LDS bytes per workgroup.
+ * Returns FDCN_EINVAL if the size is unsupported. */
+int fdcn_plan(int32_t n_nodes, int32_t it_mode, int32_t k_cap, int32_t* waves,
+              int32_t* npt, int32_t* scen_per_block, int32_t* lds_bytes);
+
+/* Extent (nodes) of the Sherman-Morrison boundary-layer correction needed by
+ * the scenarios in `params` (host memory): the largest k such that the
+ * correction at interior node k is above 1e-18 of its value at node 0, over
+ * both theta values used by the launch.  Returns a value in [1, n_nodes-2],
+ * or a negative FDCN_E* code. */
+int fdcn_sm_extent(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                   const double* params);
+
+const char* fdcn_last_error(void);
+int fdcn_device_count(void);   /* gfx950 devices visible; 0 if none          */
+int fdcn_abi_version(void);    /* FDCN_ABI_VERSION                           */
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FDCN_H */

@@ -1,0 +1,402 @@
+/*
+ * fdcn_oracle.c -- CPU ORACLE for the Crank-Nicolson hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * or the timed CPU baseline -- never as the thing measured or shipped.  The
+ * product path (finite_difference_amd) never links or calls it.
+ *
+ * Two layers:
+ *
+ *  1. oracle_ref_*: literal C restatements of the reference's time loops,
+ *     taking the reference's own inputs (grid nodes, coefficients, monitor
+ *     index set).  Every floating-point expression keeps the reference's
+ *     operand order, and the file is compiled with -ffp-contract=off, so the
+ *     results are bit-identical to the Python reference (CPython floats are
+ *     IEEE binary64, math.exp is libm exp).  tests/test_oracle_golden.py
+ *     checks that bit-for-bit against tests/golden/*.json.
+ *
+ *  2. oracle_cn_batch / oracle_it_batch: the same algorithm driven by the
+ *     C-ABI's plan arrays (include/fdcn.h), so a plan built by the product's
+ *     host code can be solved here and compared with the GPU.  Sequential
+ *     Thomas per scenario, optionally threaded over scenarios (CPU baseline).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/fdcn.h"
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ---------------------------------------------------------------------- */
+/* shared pieces                                                          */
+/* ---------------------------------------------------------------------- */
+
+/* Thomas algorithm for a constant tridiagonal system, as written at
+ * discrete_barrier_fdm_pricer.py:487-509, _cn.py:250-269 and
+ * fd_american_equity.py:625-653 (identical operation order in all three). */
+static void thomas_const(double AL, double AC, double AU, const double* rhs, int n,
+                         double* cp, double* dp, double* x) {
+  double denom = AC;
+  cp[0] = AU / denom;
+  dp[0] = rhs[0] / denom;
+  for (int i = 1; i < n; ++i) {
+    denom = AC - AL * cp[i - 1];
+    if (i < n - 1) cp[i] = AU / denom;
+    dp[i] = (rhs[i] - AL * dp[i - 1]) / denom;
+  }
+  x[n - 1] = dp[n - 1];
+  for (int i = n - 2; i >= 0; --i) x[i] = dp[i] - cp[i] * x[i + 1];
+}
+
+/* build_matrices(theta): discrete_barrier_fdm_pricer.py:475-484,
+ * fd_american_equity.py:614-623 */
+static void build_matrices(double theta, double dt, double a, double c, double bcoef,
+                           double* AL, double* AC, double* AU, double* BL, double* BC,
+                           double* BU) {
+  *AL = -theta * dt * a;
+  *AC = 1.0 - theta * dt * bcoef;
+  *AU = -theta * dt * c;
+  *BL = (1.0 - theta) * dt * a;
+  *BC = 1.0 + (1.0 - theta) * dt * bcoef;
+  *BU = (1.0 - theta) * dt * c;
+}
+
+static int in_set(const int* idx, int n, int k) {
+  for (int i = 0; i < n; ++i)
+    if (idx[i] == k) return 1;
+  return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* 1a. DiscreteBarrierFDMPricer._solve_grid                               */
+/*     discrete_barrier_fdm_pricer.py:442-547 (+ _terminal_payoff :366,  */
+/*     _boundary_values :372, _apply_KO_projection :413)                  */
+/* ---------------------------------------------------------------------- */
+/* barrier type codes */
+enum { BT_NONE = 0, BT_DOWN_OUT = 1, BT_UP_OUT = 2, BT_DOUBLE_OUT = 3, BT_KI = 4 };
+
+/* s_nodes has n_space+1 entries.  Output: V_out receives the n_space values
+ * the reference returns (its list shrinks by one on the first step). */
+int oracle_ref_barrier_solve(const double* s_nodes, int n_space, int n_time,
+                             double T, double dx, double sigma, double r, double b,
+                             double q, int rannacher_steps, int is_call, double K,
+                             int bt, int has_lo, double lo_bar, int has_up, double up_bar,
+                             double rebate_amount, int rebate_at_hit, double carry,
+                             const int* mon_idx, int n_mon, int apply_KO, double* V_out) {
+  const int N = n_space - 1;                      /* :449 */
+  const double dt = (T) / (double)n_time;         /* :452 (num_time_steps) */
+  const double sig2 = sigma * sigma;              /* :463 */
+  const double mu_x = (b - q) - 0.5 * sig2;       /* :464 */
+  const double alpha = 0.5 * sig2 / (dx * dx);    /* :467 */
+  const double beta_adv = mu_x / (2.0 * dx);      /* :468 */
+  const double a = alpha - beta_adv;
+  const double c = alpha + beta_adv;
+  const double bcoef = -2.0 * alpha - r;
+  const double S_min = s_nodes[0], S_max = s_nodes[n_space];
+
+  int len = n_space + 1;
+  double* V = (double*)malloc(sizeof(double) * (size_t)len);
+  double* rhs = (double*)malloc(sizeof(double) * (size_t)(N > 1 ? N : 2));
+  double* cp = (double*)malloc(sizeof(double) * (size_t)(N > 1 ? N : 2));
+  double* dp = (double*)malloc(sizeof(double) * (size_t)(N > 1 ? N : 2));
+  double* xs = (double*)malloc(sizeof(double) * (size_t)(N > 1 ? N : 2));
+  if (!V || !rhs || !cp || !dp || !xs) return -4;
+  for (int i = 0; i <= n_space; ++i) { /* :366-370 */
+    double v = is_call ? s_nodes[i] - K : K - s_nodes[i];
+    V[i] = (0.0 > v) ? 0.0 : v; /* Python max(v, 0.0) keeps v unless 0.0 > v */
+  }
+  int ranna = rannacher_steps;
+  for (int m = 0; m < n_time; ++m) {
+    double theta;
+    if (ranna > 0) { theta = 1.0; ranna -= 1; } else theta = 0.5;
+    double AL, AC, AU, BL, BC, BU;
+    build_matrices(theta, dt, a, c, bcoef, &AL, &AC, &AU, &BL, &BC, &BU);
+    double tau = (double)(m + 1) * dt;
+    double vmin, vmax;
+    if (is_call) { /* :386-391 */
+      vmin = 0.0;
+      vmax = S_max * exp((b - r) * tau) - K * exp(-r * tau);
+    } else {
+      vmax = 0.0;
+      vmin = K * exp(-r * tau) * S_min * exp((b - r) * tau);
+    }
+    for (int j = 1; j < N; ++j) rhs[j - 1] = BL * V[j - 1] + BC * V[j] + BU * V[j + 1];
+    rhs[0] -= AL * vmin;
+    rhs[N - 2] -= AU * vmax;
+    thomas_const(AL, AC, AU, rhs, N - 1, cp, dp, xs);
+    /* V[0]=vmin; V[-1]=vmax; V[1:-1]=x  (list length becomes N+1 = n_space) */
+    V[len - 1] = vmax;
+    double top = V[len - 1];
+    V[0] = vmin;
+    for (int i = 0; i < N - 1; ++i) V[1 + i] = xs[i];
+    len = N + 1;
+    V[len - 1] = top;
+    if (apply_KO && in_set(mon_idx, n_mon, m + 1) && bt != BT_NONE && bt != BT_KI) {
+      double reb = rebate_at_hit ? rebate_amount : rebate_amount * exp(-carry * tau);
+      int n = len < n_space + 1 ? len : n_space + 1;
+      for (int i = 0; i < n; ++i) {
+        double s = s_nodes[i];
+        int out = 0;
+        if (bt == BT_DOWN_OUT && has_lo && s <= lo_bar) out = 1;
+        else if (bt == BT_UP_OUT && has_up && s >= up_bar) out = 1;
+        else if (bt == BT_DOUBLE_OUT) {
+          if ((has_lo && s <= lo_bar) || (has_up && s >= up_bar)) out = 1;
+        }
+        if (out) V[i] = reb;
+      }
+    }
+  }
+  memcpy(V_out, V, sizeof(double) * (size_t)len);
+  free(V); free(rhs); free(cp); free(dp); free(xs);
+  return len;
+}
+
+/* ---------------------------------------------------------------------- */
+/* 1b. DiscreteBarrierCrankNicolsonLog._solve_grid                        */
+/*     discrete_barrier_fdm_pricer_cn.py:219-302                          */
+/* ---------------------------------------------------------------------- */
+int oracle_ref_cnlog_solve(const double* s_nodes, int N, int n_time, double T, double dx,
+                           double sigma, double r_disc, double b_carry, int is_call,
+                           double K, int bt, int has_lo, double lo_bar, int has_up,
+                           double up_bar, double rebate, const int* mon_idx, int n_mon,
+                           int apply_KO, double* V_out) {
+  const double dt = T / (double)n_time;
+  const double sig2 = sigma * sigma;
+  const double mu_x = b_carry - 0.5 * sig2;
+  const double alpha = 0.5 * sig2 / (dx * dx);
+  const double beta_adv = mu_x / (2.0 * dx);
+  const double a = alpha - beta_adv, c = alpha + beta_adv;
+  const double bcoef = -2.0 * alpha - r_disc;
+  const double AL = -0.5 * dt * a, AC = 1.0 - 0.5 * dt * bcoef, AU = -0.5 * dt * c;
+  const double BL = 0.5 * dt * a, BC = 1.0 + 0.5 * dt * bcoef, BU = 0.5 * dt * c;
+  const double S_max = s_nodes[N];
+  double* V = (double*)malloc(sizeof(double) * (size_t)(N + 1));
+  double* rhs = (double*)malloc(sizeof(double) * (size_t)N);
+  double* cp = (double*)malloc(sizeof(double) * (size_t)N);
+  double* dp = (double*)malloc(sizeof(double) * (size_t)N);
+  double* xs = (double*)malloc(sizeof(double) * (size_t)N);
+  if (!V || !rhs || !cp || !dp || !xs) return -4;
+  for (int i = 0; i <= N; ++i) { /* :142-151 */
+    double v = is_call ? s_nodes[i] - K : K - s_nodes[i];
+    V[i] = (0.0 > v) ? 0.0 : v; /* Python max(v, 0.0) */
+  }
+  for (int m = 0; m < n_time; ++m) {
+    double tau = (double)(m + 1) * dt;
+    double vmin, vmax;
+    if (is_call) { vmin = 0.0; vmax = S_max * exp((b_carry - r_disc) * tau) - K * exp(-r_disc * tau); }
+    else { vmax = 0.0; vmin = K * exp(-r_disc * tau); }
+    for (int j = 1; j < N; ++j) rhs[j - 1] = BL * V[j - 1] + BC * V[j] + BU * V[j + 1];
+    rhs[0] -= AL * vmin;
+    rhs[N - 2] -= AU * vmax;
+    thomas_const(AL, AC, AU, rhs, N - 1, cp, dp, xs);
+    V[0] = vmin;
+    V[N] = vmax;
+    for (int i = 0; i < N - 1; ++i) V[1 + i] = xs[i];
+    if (apply_KO && in_set(mon_idx, n_mon, m + 1)) { /* :199-213 */
+      if (bt == BT_DOWN_OUT && has_lo) {
+        for (int i = 0; i <= N; ++i) if (s_nodes[i] <= lo_bar) V[i] = rebate;
+      } else if (bt == BT_UP_OUT && has_up) {
+        for (int i = 0; i <= N; ++i) if (s_nodes[i] >= up_bar) V[i] = rebate;
+      }
+    }
+  }
+  memcpy(V_out, V, sizeof(double) * (size_t)(N + 1));
+  free(V); free(rhs); free(cp); free(dp); free(xs);
+  return N + 1;
+}
+
+/* ---------------------------------------------------------------------- */
+/* 1c. AmericanFDMPricer._solve_segment                                   */
+/*     fd_american_equity.py:559-726 (+ _boundary_values :430-448)        */
+/* ---------------------------------------------------------------------- */
+int oracle_ref_american_segment(const double* s_nodes, int n_space, double dx,
+                                const double* v_init, double tau_start, double tau_end,
+                                int n_steps, int restart_rannacher, int rannacher_steps,
+                                double sigma, double r, double b, int is_call,
+                                double strike_pde, double* v_out) {
+  if (n_steps < 1) { memcpy(v_out, v_init, sizeof(double) * (size_t)(n_space + 1)); return 0; }
+  const double dt = (tau_end - tau_start) / (double)n_steps;
+  const double sigma_sq = sigma * sigma;
+  const double q = 0.0;
+  const double mu_x = (b - q) - 0.5 * sigma_sq;
+  const double alpha = 0.5 * sigma_sq / (dx * dx);
+  const double beta_adv = mu_x / (2.0 * dx);
+  const double a_coef = alpha - beta_adv, c_coef = alpha + beta_adv;
+  const double b_coef = -2.0 * alpha - r;
+  const int n = n_space - 1;
+  const double s_max = s_nodes[n_space];
+  double* v = (double*)malloc(sizeof(double) * (size_t)(n_space + 1));
+  double* lam = (double*)calloc((size_t)n, sizeof(double));
+  double* pay = (double*)malloc(sizeof(double) * (size_t)n);
+  double* rhs = (double*)malloc(sizeof(double) * (size_t)n);
+  double* cp = (double*)malloc(sizeof(double) * (size_t)n);
+  double* dp = (double*)malloc(sizeof(double) * (size_t)n);
+  double* xs = (double*)malloc(sizeof(double) * (size_t)n);
+  if (!v || !lam || !pay || !rhs || !cp || !dp || !xs) return -4;
+  memcpy(v, v_init, sizeof(double) * (size_t)(n_space + 1));
+  for (int k = 0; k < n; ++k) { /* _intrinsic_payoff :419-424 at interior nodes */
+    double s = s_nodes[k + 1];
+    double e = is_call ? s - strike_pde : strike_pde - s;
+    pay[k] = (0.0 > e) ? 0.0 : e;
+  }
+  const int base_ranna = restart_rannacher ? rannacher_steps : 0;
+  double tau = tau_start;
+  for (int step = 0; step < n_steps; ++step) {
+    double tau_next = tau + dt;
+    double theta = step < base_ranna ? 1.0 : 0.5;
+    double al, ac, au, bl, bc, bu;
+    build_matrices(theta, dt, a_coef, c_coef, b_coef, &al, &ac, &au, &bl, &bc, &bu);
+    double vmin, vmax;
+    if (is_call) { vmin = 0.0; vmax = s_max * exp((b - r) * tau_next) - strike_pde * exp(-r * tau_next); }
+    else { vmin = strike_pde * exp(-r * tau_next); vmax = 0.0; }
+    for (int j = 1; j < n_space; ++j)
+      rhs[j - 1] = bl * v[j - 1] + bc * v[j] + bu * v[j + 1] + dt * lam[j - 1];
+    rhs[0] -= al * vmin;
+    rhs[n - 1] -= au * vmax;
+    thomas_const(al, ac, au, rhs, n, cp, dp, xs);
+    for (int k = 0; k < n; ++k) { /* :704-717 */
+      double tv = xs[k], pk = pay[k], lo = lam[k];
+      double cand = tv - dt * lo;
+      double vn = pk > cand ? pk : cand;
+      double ln = lo + (pk - tv) / dt;
+      if (ln < 0.0) ln = 0.0;
+      lam[k] = ln;
+      xs[k] = vn;
+    }
+    v[0] = vmin;
+    v[n_space] = vmax;
+    for (int k = 0; k < n; ++k) v[1 + k] = xs[k];
+    tau = tau_next;
+  }
+  memcpy(v_out, v, sizeof(double) * (size_t)(n_space + 1));
+  free(v); free(lam); free(pay); free(rhs); free(cp); free(dp); free(xs);
+  return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* 2. plan-level solvers (same arguments as fdcn_cn_batch / fdcn_it_batch) */
+/* ---------------------------------------------------------------------- */
+static double bnd_value(int form, double c0, double e0, double c1, double e1, double tau) {
+  if (form == 1) return c0 * exp(e0 * tau) * c1 * exp(e1 * tau);
+  return c0 * exp(e0 * tau) + c1 * exp(e1 * tau);
+}
+
+static void plan_solve_one(int it_mode, int n_nodes, int n_time, int n_ranna,
+                           const double* P, const int32_t* I, const double* v_init,
+                           const double* payoff, const int32_t* mon_step,
+                           const double* mon_rebate, double* v_out, double* work) {
+  const int n = n_nodes - 2;
+  double* V = work;
+  double* rhs = V + n_nodes;
+  double* cp = rhs + n;
+  double* dp = cp + n;
+  double* xs = dp + n;
+  double* lam = xs + n;
+  memcpy(V, v_init, sizeof(double) * (size_t)n_nodes);
+  if (it_mode) memset(lam, 0, sizeof(double) * (size_t)n);
+  const double dt = P[FDCN_P_DT], a = P[FDCN_P_A], c = P[FDCN_P_C], bcoef = P[FDCN_P_BC];
+  int mon_pos = I[FDCN_I_MON_START];
+  const int mon_end = mon_pos + I[FDCN_I_MON_COUNT];
+  const int ko_lo = I[FDCN_I_KO_LO], ko_hi = I[FDCN_I_KO_HI];
+  double tau = P[FDCN_P_TAU0];
+  for (int m = 0; m < n_time; ++m) {
+    const double theta = m < n_ranna ? 1.0 : 0.5;
+    double AL, AC, AU, BL, BC, BU;
+    build_matrices(theta, dt, a, c, bcoef, &AL, &AC, &AU, &BL, &BC, &BU);
+    if (I[FDCN_I_TAU_MODE] == 1) tau = tau + dt;
+    else tau = P[FDCN_P_TAU0] + (double)(m + 1) * dt;
+    const double lo = bnd_value(I[FDCN_I_LO_FORM], P[FDCN_P_LO_C0], P[FDCN_P_LO_E0],
+                                P[FDCN_P_LO_C1], P[FDCN_P_LO_E1], tau);
+    const double hi = bnd_value(I[FDCN_I_HI_FORM], P[FDCN_P_HI_C0], P[FDCN_P_HI_E0],
+                                P[FDCN_P_HI_C1], P[FDCN_P_HI_E1], tau);
+    if (it_mode)
+      for (int j = 1; j <= n; ++j)
+        rhs[j - 1] = BL * V[j - 1] + BC * V[j] + BU * V[j + 1] + dt * lam[j - 1];
+    else
+      for (int j = 1; j <= n; ++j) rhs[j - 1] = BL * V[j - 1] + BC * V[j] + BU * V[j + 1];
+    rhs[0] -= AL * lo;
+    rhs[n - 1] -= AU * hi;
+    thomas_const(AL, AC, AU, rhs, n, cp, dp, xs);
+    if (it_mode) {
+      for (int k = 0; k < n; ++k) {
+        double tv = xs[k], pk = payoff[k + 1], lo_ = lam[k];
+        double cand = tv - dt * lo_;
+        double ln = lo_ + (pk - tv) / dt;
+        if (ln < 0.0) ln = 0.0;
+        lam[k] = ln;
+        xs[k] = pk > cand ? pk : cand;
+      }
+    }
+    V[0] = lo;
+    V[n_nodes - 1] = hi;
+    memcpy(V + 1, xs, sizeof(double) * (size_t)n);
+    if (mon_pos < mon_end && mon_step[mon_pos] == m + 1) {
+      const double reb = mon_rebate[mon_pos];
+      for (int j = 0; j < n_nodes; ++j)
+        if (j <= ko_lo || j >= ko_hi) V[j] = reb;
+      ++mon_pos;
+    }
+    while (mon_pos < mon_end && mon_step[mon_pos] <= m + 1) ++mon_pos;
+  }
+  memcpy(v_out, V, sizeof(double) * (size_t)n_nodes);
+}
+
+static int plan_batch(int it_mode, int32_t B, int32_t n_nodes, int32_t n_time,
+                      int32_t n_ranna, const double* params, const int32_t* iparams,
+                      const double* v_init, const double* payoff, const int32_t* mon_step,
+                      const double* mon_rebate, double* v_out, int nthreads) {
+  if (B < 0 || n_nodes < 4 || n_time < 0) return FDCN_EINVAL;
+  const size_t wlen = (size_t)n_nodes + 5 * (size_t)n_nodes;
+  int err = 0;
+#ifdef _OPENMP
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+  {
+    double* work = (double*)malloc(sizeof(double) * wlen);
+    if (!work) {
+      err = FDCN_ENOMEM;
+    } else {
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+      for (int32_t bi = 0; bi < B; ++bi)
+        plan_solve_one(it_mode, n_nodes, n_time, n_ranna, params + (size_t)bi * FDCN_NPARAM,
+                       iparams + (size_t)bi * FDCN_NIPARAM, v_init + (size_t)bi * n_nodes,
+                       it_mode ? payoff + (size_t)bi * n_nodes : NULL, mon_step, mon_rebate,
+                       v_out + (size_t)bi * n_nodes, work);
+      free(work);
+    }
+  }
+  (void)nthreads;
+  return err;
+}
+
+int oracle_cn_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                    const double* params, const int32_t* iparams, const double* v_init,
+                    int32_t n_mon, const int32_t* mon_step, const double* mon_rebate,
+                    double* v_out, int32_t nthreads) {
+  (void)n_mon;
+  return plan_batch(0, B, n_nodes, n_time, n_ranna, params, iparams, v_init, NULL, mon_step,
+                    mon_rebate, v_out, nthreads);
+}
+
+int oracle_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                    const double* params, const int32_t* iparams, const double* v_init,
+                    const double* payoff, double* v_out, int32_t nthreads) {
+  return plan_batch(1, B, n_nodes, n_time, n_ranna, params, iparams, v_init, payoff, NULL,
+                    NULL, v_out, nthreads);
+}
+
+int oracle_max_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
