@@ -1,0 +1,560 @@
+"""American vanilla pricer: CN + Rannacher + Ikonen-Toivanen in log-spot.
+
+Drop-in for ``AmericanFDMPricer`` (fd_american_equity.py:42-1068; the twin
+file fd_american_option_pricer.py computes bit-identical numbers).  Same
+constructor arguments, same public methods (``price_log``, ``price_log2``,
+``greeks_log2``) and the same numerics; the difference is where the time
+march runs:
+
+* every ``_solve_segment`` (fd_american_equity.py:559-726) becomes one
+  scenario of a batched Ikonen-Toivanen launch on the MI355X
+  (libfdcn ``fdcn_it_batch``);
+* ``price_log2`` + ``greeks_log2`` need up to 8 grid solves (N, 2*num_space
+  _nodes, 2N, sigma +-h, +-2h); the unique ones are solved together, segment
+  by segment in lock-step, and cached, so the pair costs 2 launches instead
+  of 8 sequential Python marches.
+
+Discrete dividends keep the reference's host-side natural-cubic-spline jump
+(fd_american_equity.py:479-553, 732-772) between segment launches.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import math
+from typing import Dict, List, Literal, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import market
+from .engine import FORM_SUM, Boundary, Engine, Solve, default_engine, operator_coefficients
+
+OptionType = Literal["call", "put"]
+
+
+def _pmax(x: float, y: float) -> float:
+    """Python's max(x, y) (keeps x unless y > x)."""
+    return y if y > x else x
+
+
+class AmericanFDMPricer:
+    """American vanilla option, Crank-Nicolson in log S with IT early exercise."""
+
+    def __init__(
+        self,
+        spot: float,
+        strike: float,
+        valuation_date: _dt.date,
+        maturity_date: _dt.date,
+        sigma: float,
+        option_type: OptionType,
+        discount_curve,
+        forward_curve=None,
+        dividend_schedule: Optional[List[Tuple[_dt.date, float]]] = None,
+        trade_id: Optional[int] = None,
+        direction: str = "long",
+        quantity: int = 1,
+        contract_multiplier: float = 1.0,
+        underlying_spot_days: int = 0,
+        option_days: int = 0,
+        option_settlement_days: int = 0,
+        day_count: str = "ACT/365",
+        grid_type: str = "uniform",
+        num_space_nodes: int = 400,
+        num_time_steps: int = 400,
+        rannacher_steps: int = 2,
+        s_max_mult: float = 4.5,
+        engine: Optional[Engine] = None,
+    ) -> None:
+        if spot <= 0.0 or strike <= 0.0 or sigma <= 0.0:
+            raise ValueError("spot, strike and sigma must be positive.")
+        if maturity_date <= valuation_date:
+            raise ValueError("maturity_date must be after valuation_date.")
+        self.spot = float(spot)
+        self.strike = float(strike)
+        self.valuation_date = valuation_date
+        self.maturity_date = maturity_date
+        self.sigma = float(sigma)
+        self.option_type: str = option_type.lower()
+        if self.option_type not in ("call", "put"):
+            raise ValueError("option_type must be 'call' or 'put'.")
+
+        self.discount_curve_df = discount_curve.copy()
+        self.forward_curve_df = forward_curve.copy() if forward_curve is not None else None
+        self._curve = market.NacaCurve(self.discount_curve_df)
+        self.dividend_schedule = sorted(dividend_schedule or [], key=lambda x: x[0])
+
+        self.trade_id = trade_id
+        self.direction = direction
+        self.quantity = int(quantity)
+        self.contract_multiplier = float(contract_multiplier)
+
+        self.calendar = market.SouthAfrica()
+        self.underlying_spot_days = int(underlying_spot_days)
+        self.option_days = int(option_days)
+        self.option_settlement_days = int(option_settlement_days)
+
+        self.day_count = market.normalise_day_count(day_count)
+        self._year_denominator = market.year_denominator(self.day_count)
+        self.grid_type = grid_type.lower()
+
+        cal = self.calendar
+        self.carry_start_date = cal.add_working_days(valuation_date, self.underlying_spot_days)
+        self.carry_end_date = cal.add_working_days(maturity_date, self.underlying_spot_days)
+        self.discount_start_date = cal.add_working_days(valuation_date, self.option_days)
+        self.discount_end_date = cal.add_working_days(maturity_date, self.option_settlement_days)
+
+        self.time_to_expiry = self._year_fraction(valuation_date, maturity_date)
+        self.time_to_carry = self._year_fraction(self.carry_start_date, self.carry_end_date)
+        self.time_to_discount = self._year_fraction(self.discount_start_date,
+                                                    self.discount_end_date)
+        if self.time_to_expiry <= 0.0:
+            raise ValueError("time_to_expiry must be positive.")
+
+        self.discount_rate_nacc = self.get_forward_nacc_rate(self.discount_start_date,
+                                                             self.discount_end_date)
+        # fd_american_equity.py:235-240: the carry rate is read off the discount
+        # curve over the carry window whenever a forward curve is supplied.
+        if self.forward_curve_df is not None:
+            self.carry_rate_nacc = self.get_forward_nacc_rate(self.carry_start_date,
+                                                              self.carry_end_date)
+        else:
+            self.carry_rate_nacc = self.discount_rate_nacc
+        self.div_yield_nacc = 0.0
+
+        self.num_space_nodes = max(int(num_space_nodes), 3)
+        self.num_time_steps = max(int(num_time_steps), 4)
+        self.rannacher_steps = max(int(rannacher_steps), 0)
+        self.s_max_mult = float(s_max_mult)
+
+        self.snap_spot_to_grid: bool = True
+        self.snap_strike_to_grid: bool = True
+        self.spot_grid_index: Optional[int] = None
+        self.spot_snapped: Optional[float] = None
+        self.strike_grid_index: Optional[int] = None
+        self.strike_snapped: Optional[float] = None
+
+        self.s_nodes: List[float] = []
+        self.x_nodes: List[float] = []
+        self._S_min = 0.0
+        self._S_max = 0.0
+        self._dx = 0.0
+
+        self.engine = engine
+        self._cache: Dict[tuple, Tuple[np.ndarray, dict]] = {}
+
+    # ------------------------------------------------------------------ dates
+    def _infer_denominator(self, day_count: str) -> int:
+        return market.year_denominator(day_count)
+
+    def _year_fraction(self, start_date: _dt.date, end_date: _dt.date) -> float:
+        return market.year_fraction(self.day_count, start_date, end_date)
+
+    def get_discount_factor(self, lookup_date: _dt.date) -> float:
+        return market.discount_factor(self._curve, self.day_count, self.valuation_date,
+                                      lookup_date)
+
+    def get_forward_nacc_rate(self, start_date: _dt.date, end_date: _dt.date) -> float:
+        return market.forward_nacc(self._curve, self.day_count, self.valuation_date,
+                                   start_date, end_date)
+
+    # ------------------------------------------------------------------- grid
+    def _configure_grid(self) -> None:
+        """Log-S band around sqrt(S K) (fd_american_equity.py:340-361)."""
+        T = self.time_to_expiry
+        sig = self.sigma
+        s_low = min(self.spot, self.strike)
+        s_high = max(self.spot, self.strike)
+        s_c = math.sqrt(max(s_low * s_high, 1e-12))
+        band = self.s_max_mult * sig * math.sqrt(max(T, 1e-12))
+        x_c = math.log(s_c)
+        s_min = math.exp(x_c - 0.5 * band)
+        s_max = math.exp(x_c + 0.5 * band)
+        s_min = min(s_min, 0.5 * s_low)
+        s_max = max(s_max, 2.0 * s_high)
+        self._S_min = max(s_min, 1e-8)
+        self._S_max = s_max
+
+    def _build_log_grid(self) -> float:
+        """Uniform log grid + critical-level snapping (fd_american_equity.py:363-407)."""
+        self._configure_grid()
+        x_min = math.log(self._S_min)
+        x_max = math.log(self._S_max)
+        n = self.num_space_nodes
+        dx = (x_max - x_min) / float(n)
+        self.x_nodes = [x_min + i * dx for i in range(n + 1)]
+        self.s_nodes = list(map(math.exp, self.x_nodes))
+        self._dx = dx
+        self._snap_critical_levels_to_grid()
+        return dx
+
+    def _snap_critical_levels_to_grid(self) -> None:
+        s = np.asarray(self.s_nodes)
+        if s.size == 0:
+            return
+        if self.snap_spot_to_grid:
+            i = int(np.argmin(np.abs(s - self.spot)))
+            self.spot_grid_index, self.spot_snapped = i, self.s_nodes[i]
+        else:
+            self.spot_grid_index = self.spot_snapped = None
+        if self.snap_strike_to_grid:
+            i = int(np.argmin(np.abs(s - self.strike)))
+            self.strike_grid_index, self.strike_snapped = i, self.s_nodes[i]
+        else:
+            self.strike_grid_index = self.strike_snapped = None
+
+    # ------------------------------------------------------- payoff / bounds
+    def _strike_for_pde(self) -> float:
+        if self.snap_strike_to_grid and self.strike_snapped is not None:
+            return self.strike_snapped
+        return self.strike
+
+    def _intrinsic_payoff(self, spot: float) -> float:
+        k = self._strike_for_pde()
+        if self.option_type == "call":
+            return _pmax(spot - k, 0.0)
+        return _pmax(k - spot, 0.0)
+
+    def _payoff_array(self) -> np.ndarray:
+        """Vectorised _intrinsic_payoff over the grid; np.where(0.0 > e, 0.0, e)
+        is exactly Python's max(e, 0.0)."""
+        s = np.asarray(self.s_nodes, dtype=np.float64)
+        k = self._strike_for_pde()
+        e = s - k if self.option_type == "call" else k - s
+        return np.where(0.0 > e, 0.0, e)
+
+    def _terminal_payoff(self) -> List[float]:
+        return self._payoff_array().tolist()
+
+    def _boundary_values(self, tau: float) -> Tuple[float, float]:
+        lo, hi = self._boundaries()
+        return lo.value(tau), hi.value(tau)
+
+    def _boundaries(self) -> Tuple[Boundary, Boundary]:
+        """Dirichlet values of fd_american_equity.py:430-448 as kernel forms."""
+        r, b = self.discount_rate_nacc, self.carry_rate_nacc
+        k = self._strike_for_pde()
+        if self.option_type == "call":
+            return Boundary(), Boundary(FORM_SUM, self.s_nodes[-1], b - r, -k, -r)
+        return Boundary(FORM_SUM, k, -r, 0.0, 0.0), Boundary()
+
+    # -------------------------------------------------------------- dividends
+    def _div_times_tau(self) -> List[Tuple[float, float]]:
+        """(tau_div, cash) of dividends strictly inside (valuation, maturity)."""
+        out = []
+        for pay_date, amount in self.dividend_schedule:
+            if self.valuation_date < pay_date < self.maturity_date:
+                t_rel = self._year_fraction(self.valuation_date, pay_date)
+                if 0.0 < t_rel < self.time_to_expiry:
+                    out.append((self.time_to_expiry - t_rel, float(amount)))
+        out.sort(key=lambda x: x[0])
+        return out
+
+    @staticmethod
+    def _build_natural_cubic_spline(x: Sequence[float], y: Sequence[float]):
+        """Natural cubic spline S(x) (fd_american_equity.py:479-553), returned
+        as a vectorised evaluator with the same arithmetic per point."""
+        xa = np.asarray(x, dtype=float)
+        ya = np.asarray(y, dtype=float)
+        n = xa.size
+        if n < 2:
+            raise ValueError("Need at least two points for spline.")
+        h = np.diff(xa)
+        if np.any(h <= 0.0):
+            raise ValueError("x must be strictly increasing.")
+        alpha = np.zeros(n)
+        dy = ya[1:] - ya[:-1]
+        alpha[1:-1] = 3.0 / h[1:] * dy[1:] - 3.0 / h[:-1] * dy[:-1]
+        l_ = np.ones(n)
+        mu = np.zeros(n)
+        z = np.zeros(n)
+        for i in range(1, n - 1):
+            l_[i] = 2.0 * (xa[i + 1] - xa[i - 1]) - h[i - 1] * mu[i - 1]
+            mu[i] = h[i] / l_[i]
+            z[i] = (alpha[i] - h[i - 1] * z[i - 1]) / l_[i]
+        c = np.zeros(n)
+        b = np.zeros(n - 1)
+        d = np.zeros(n - 1)
+        for j in range(n - 2, -1, -1):
+            c[j] = z[j] - mu[j] * c[j + 1]
+            b[j] = (ya[j + 1] - ya[j]) / h[j] - h[j] * (c[j + 1] + 2.0 * c[j]) / 3.0
+            d[j] = (c[j + 1] - c[j]) / (3.0 * h[j])
+        a = ya[:-1]
+
+        def evaluate(q: np.ndarray) -> np.ndarray:
+            q = np.asarray(q, dtype=float)
+            j = np.searchsorted(xa, q, side="right") - 1
+            j = np.where(q <= xa[0], 0, np.where(q >= xa[-1], n - 2, j))
+            t = q - xa[j]
+            return a[j] + b[j] * t + c[j] * t * t + d[j] * t * t * t
+
+        return evaluate
+
+    def _apply_dividend_jump(self, v_after: Sequence[float], cash_div: float) -> List[float]:
+        """V(t_d-, S) = V(t_d+, S - D), plus exercise for calls (…equity.py:732-772)."""
+        s = np.asarray(self.s_nodes)
+        v = np.asarray(v_after, dtype=float)
+        spline = self._build_natural_cubic_spline(s, v)
+        q = s - cash_div
+        cont = np.where(q <= s[0], v[0], np.where(q >= s[-1], v[-1], spline(q)))
+        if self.option_type == "call":
+            k = self._strike_for_pde()
+            ex = np.array([_pmax(x - k, 0.0) for x in s])
+            return [_pmax(float(cv), float(e)) for cv, e in zip(cont, ex)]
+        return [float(x) for x in cont]
+
+    # ------------------------------------------------------------ the solves
+    def _segment_solve(self, v_init: Sequence[float], tau_start: float, tau_end: float,
+                       n_steps: int, restart_rannacher: bool) -> Solve:
+        """The work of one _solve_segment call as a kernel scenario."""
+        dt = (tau_end - tau_start) / float(n_steps)
+        coeffs = operator_coefficients(self.sigma, self.carry_rate_nacc, 0.0,
+                                       self.discount_rate_nacc, self._dx)
+        lower, upper = self._boundaries()
+        pay = self._payoff_array()
+        return Solve(it=True, n_time=int(n_steps),
+                     n_ranna=self.rannacher_steps if restart_rannacher else 0, dt=dt,
+                     coeffs=coeffs, v_init=np.asarray(v_init, dtype=np.float64), lower=lower,
+                     upper=upper, tau0=tau_start, tau_accumulate=True, payoff=pay)
+
+    def _engine(self) -> Engine:
+        return self.engine if self.engine is not None else default_engine()
+
+    def _solve_segment(self, v_init: List[float], tau_start: float, tau_end: float,
+                       n_steps: int, restart_rannacher: bool) -> List[float]:
+        """fd_american_equity.py:559-726 on the GPU (one-scenario launch)."""
+        if n_steps < 1:
+            return v_init
+        if len(self.s_nodes) - 1 < 2:
+            raise RuntimeError("Spatial grid too coarse.")
+        s = self._segment_solve(v_init, tau_start, tau_end, n_steps, restart_rannacher)
+        return self._engine().run([s])[0].tolist()
+
+    def _segments(self, n_time: int):
+        total_tau = self.time_to_expiry
+        divs = self._div_times_tau()
+        base_n = int(n_time)
+        base_dt = total_tau / float(base_n)
+        pts = [0.0] + [t for t, _ in divs] + [total_tau]
+        steps: List[int] = []
+        remaining = base_n
+        for i in range(len(pts) - 2):
+            ns = max(1, int(round((pts[i + 1] - pts[i]) / base_dt)))
+            steps.append(ns)
+            remaining -= ns
+        steps.append(max(1, remaining))
+        return divs, pts, steps
+
+    def _state_key(self, sigma: float, n_time: int) -> tuple:
+        return (float(sigma), int(n_time), self.spot, self.strike, self.time_to_expiry,
+                self.discount_rate_nacc, self.carry_rate_nacc, self.num_space_nodes,
+                self.rannacher_steps, self.s_max_mult, self.option_type,
+                tuple(self.dividend_schedule), self.snap_spot_to_grid, self.snap_strike_to_grid)
+
+    def _grid_state(self) -> dict:
+        return dict(s_nodes=self.s_nodes, x_nodes=self.x_nodes, _S_min=self._S_min,
+                    _S_max=self._S_max, _dx=self._dx, spot_grid_index=self.spot_grid_index,
+                    spot_snapped=self.spot_snapped, strike_grid_index=self.strike_grid_index,
+                    strike_snapped=self.strike_snapped)
+
+    def _restore(self, st: dict) -> None:
+        for k, v in st.items():
+            setattr(self, k, v)
+
+    def prefetch(self, requests: Sequence[Tuple[float, int]]) -> None:
+        """Solve the (sigma, n_time) grids not yet cached, all together.
+
+        Segments are marched in lock-step: every pending request's segment i
+        goes into one batched launch (grouped by step count), then the host
+        applies the dividend jump, then segment i+1."""
+        pending = []
+        seen = set()
+        for sig, nt in requests:
+            key = self._state_key(sig, nt)
+            if key in self._cache or key in seen:
+                continue
+            seen.add(key)
+            pending.append((key, float(sig), int(nt)))
+        if not pending:
+            return
+        sigma0 = self.sigma
+        saved = self._grid_state()
+        jobs = []
+        try:
+            for key, sig, nt in pending:
+                self.sigma = sig
+                self._build_log_grid()
+                divs, pts, steps = self._segments(nt)
+                jobs.append(dict(key=key, sigma=sig, grid=self._grid_state(), divs=divs,
+                                 pts=pts, steps=steps, v=self._payoff_array()))
+            n_seg = max(len(j["steps"]) for j in jobs)
+            for seg in range(n_seg):
+                solves, owners = [], []
+                for j in jobs:
+                    if seg >= len(j["steps"]):
+                        continue
+                    self.sigma = j["sigma"]
+                    self._restore(j["grid"])
+                    restart = seg == 0 or (seg > 0 and self.option_type == "call")
+                    ns = j["steps"][seg]
+                    if ns < 1:
+                        continue
+                    solves.append(self._segment_solve(j["v"], j["pts"][seg], j["pts"][seg + 1],
+                                                      ns, restart))
+                    owners.append(j)
+                if solves:
+                    if len(self.s_nodes) - 1 < 2:
+                        raise RuntimeError("Spatial grid too coarse.")
+                    for j, v in zip(owners, self._engine().run(solves)):
+                        j["v"] = v
+                for j in jobs:
+                    if seg < len(j["divs"]):
+                        self.sigma = j["sigma"]
+                        self._restore(j["grid"])
+                        j["v"] = self._apply_dividend_jump(j["v"], j["divs"][seg][1])
+            for j in jobs:
+                self._cache[j["key"]] = (np.asarray(j["v"], dtype=np.float64), j["grid"])
+        finally:
+            self.sigma = sigma0
+            self._restore(saved)
+
+    def _solve_grid(self, n_time: Optional[int] = None) -> List[float]:
+        """Value vector at valuation (fd_american_equity.py:778-843)."""
+        nt = self.num_time_steps if n_time is None else int(n_time)
+        self.prefetch([(self.sigma, nt)])
+        V, grid = self._cache[self._state_key(self.sigma, nt)]
+        self._restore(grid)
+        return V.tolist()
+
+    # ----------------------------------------------------- price and greeks
+    def _spot_for_interp(self) -> float:
+        if self.snap_spot_to_grid and self.spot_snapped is not None:
+            return self.spot_snapped
+        return self.spot
+
+    def _interp_price(self, v_values: Sequence[float]) -> float:
+        s = self.s_nodes
+        s0 = self._spot_for_interp()
+        if s0 <= s[0]:
+            return float(v_values[0])
+        if s0 >= s[-1]:
+            return float(v_values[-1])
+        hi = int(np.searchsorted(np.asarray(s), s0, side="right"))
+        lo = hi - 1
+        w = (s0 - s[lo]) / (s[hi] - s[lo])
+        return float((1.0 - w) * v_values[lo] + w * v_values[hi])
+
+    def _local_cubic_delta_gamma(self, v_values: Sequence[float]) -> Tuple[float, float]:
+        """Four-point cubic fit around the snapped spot (…equity.py:876-907)."""
+        s = self.s_nodes
+        s0 = self._spot_for_interp()
+        n = len(s) - 1
+        i = int(np.argmin(np.abs(np.asarray(s) - s0)))
+        i = 1 if i < 1 else (n - 2 if i > n - 2 else i)
+        idx = [i - 1, i, i + 1, i + 2]
+        xv = np.array([s[j] for j in idx], dtype=float)
+        yv = np.array([v_values[j] for j in idx], dtype=float)
+        z = xv - s0
+        design = np.vstack([z ** 3, z ** 2, z, np.ones_like(z)]).T
+        _, b_coef, c_coef, _ = np.linalg.solve(design, yv)
+        return float(c_coef), float(2.0 * b_coef)
+
+    def price_log(self, n_time: Optional[int] = None) -> float:
+        return self._interp_price(self._solve_grid(n_time=n_time))
+
+    def price_log2(self, apply_ko: bool = True, use_richardson: bool = True) -> float:
+        """Richardson N vs 2*num_space_nodes (the reference's quirk, :950)."""
+        if not use_richardson:
+            return self.price_log(n_time=self.num_time_steps)
+        self.prefetch([(self.sigma, self.num_time_steps), (self.sigma, 2 * self.num_space_nodes)])
+        p_n = self.price_log(n_time=self.num_time_steps)
+        p_2n = self.price_log(n_time=2 * self.num_space_nodes)
+        return (4.0 * p_2n - p_n) / 3.0
+
+    def _price_for_sigma(self, sigma: float, n_time: Optional[int] = None) -> float:
+        original = self.sigma
+        try:
+            self.sigma = sigma
+            return self.price_log(n_time=n_time)
+        finally:
+            self.sigma = original
+
+    def greeks_requests(self, dv_sigma: float = 0.01, use_richardson: bool = True,
+                        with_price: bool = True):
+        """(sigma, n_time) grids price_log2 + greeks_log2 will ask for."""
+        N, s0, h = self.num_time_steps, self.sigma, dv_sigma
+        req = [(s0, N)]
+        if use_richardson:
+            req += [(s0, 2 * N), (s0 + h, N), (s0 - h, N), (s0 + 2.0 * h, N), (s0 - 2.0 * h, N)]
+            if with_price:
+                req.append((s0, 2 * self.num_space_nodes))
+        else:
+            req += [(s0 + h, N), (s0 - h, N)]
+        return req
+
+    def greeks_log2(self, dv_sigma: float = 0.01, use_richardson: bool = True) -> Dict[str, float]:
+        """Price and Greeks as fd_american_equity.py:970-1068."""
+        self.prefetch(self.greeks_requests(dv_sigma, use_richardson, with_price=False))
+        v_n = self._solve_grid(n_time=self.num_time_steps)
+        price_n = self._interp_price(v_n)
+        delta_n, gamma_n = self._local_cubic_delta_gamma(v_n)
+        if use_richardson:
+            v_2n = self._solve_grid(n_time=2 * self.num_time_steps)
+            price_2n = self._interp_price(v_2n)
+            delta_2n, gamma_2n = self._local_cubic_delta_gamma(v_2n)
+            price = (4.0 * price_2n - price_n) / 3.0
+            delta = (4.0 * delta_2n - delta_n) / 3.0
+            gamma = (4.0 * gamma_2n - gamma_n) / 3.0
+        else:
+            price, delta, gamma = price_n, delta_n, gamma_n
+        sigma0 = self.sigma
+        h = dv_sigma
+        N = self.num_time_steps
+        if use_richardson:
+            first_h = (self._price_for_sigma(sigma0 + h, N)
+                       - self._price_for_sigma(sigma0 - h, N)) / (2.0 * h)
+            first_2h = (self._price_for_sigma(sigma0 + 2.0 * h, N)
+                        - self._price_for_sigma(sigma0 - 2.0 * h, N)) / (4.0 * h)
+            dvds = (4.0 * first_h - first_2h) / 3.0
+        else:
+            dvds = (self._price_for_sigma(sigma0 + h, N)
+                    - self._price_for_sigma(sigma0 - h, N)) / (2.0 * h)
+        vega = dvds / 100.0
+        r, b, q, s0 = self.discount_rate_nacc, self.carry_rate_nacc, 0.0, self.spot
+        theta = -(0.5 * sigma0 * sigma0 * s0 * s0 * gamma + (b - q) * s0 * delta - r * price)
+        return {"price": float(price), "delta": float(delta), "gamma": float(gamma),
+                "vega": float(vega), "theta": float(theta)}
+
+
+def prefetch_many(pricers: Sequence[AmericanFDMPricer], dv_sigma: float = 0.01,
+                  use_richardson: bool = True) -> None:
+    """Solve every grid that price_log2 + greeks_log2 of many trades will need.
+
+    Trades without dividends are a single segment each: all their unique
+    (sigma, n_time) grids go into one engine.run (one launch per distinct
+    (n_nodes, n_time)).  Trades with dividends are prefetched per trade
+    (segment lock-step across that trade's grids)."""
+    if not pricers:
+        return
+    engine = pricers[0]._engine()
+    solves, owners = [], []
+    for p in pricers:
+        if p._div_times_tau():
+            p.prefetch(p.greeks_requests(dv_sigma, use_richardson))
+            continue
+        sigma0, saved = p.sigma, p._grid_state()
+        seen = set()
+        for sig, nt in p.greeks_requests(dv_sigma, use_richardson):
+            key = p._state_key(sig, nt)
+            if key in p._cache or key in seen:
+                continue
+            seen.add(key)
+            p.sigma = sig
+            p._build_log_grid()
+            solves.append(p._segment_solve(p._payoff_array(), 0.0, p.time_to_expiry,
+                                           int(nt), True))
+            owners.append((p, key, p._grid_state()))
+        p.sigma = sigma0
+        p._restore(saved)
+    if solves:
+        for (p, key, grid), v in zip(owners, engine.run(solves)):
+            p._cache[key] = (np.asarray(v, dtype=np.float64), grid)

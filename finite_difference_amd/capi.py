@@ -1,0 +1,170 @@
+"""ctypes binding of libfdcn.so (include/fdcn.h).
+
+This is the product's only route to the time-stepping hot path.  There is no
+CPU fallback: if the library is missing, or no gfx950 device is visible when a
+solve is requested, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(HERE, "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libfdcn.so")
+REPO_ROOT = os.path.dirname(HERE)
+HEADER_PATH = os.path.join(REPO_ROOT, "include", "fdcn.h")
+
+# mirrors of the enums in include/fdcn.h
+P_DT, P_A, P_C, P_BC, P_TAU0 = 0, 1, 2, 3, 4
+P_LO_C0, P_LO_E0, P_LO_C1, P_LO_E1 = 5, 6, 7, 8
+P_HI_C0, P_HI_E0, P_HI_C1, P_HI_E1 = 9, 10, 11, 12
+NPARAM = 13
+I_LO_FORM, I_HI_FORM, I_KO_LO, I_KO_HI, I_MON_START, I_MON_COUNT, I_TAU_MODE = range(7)
+NIPARAM = 7
+ABI_VERSION = 1
+
+EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batch_dev",
+            "fdcn_plan", "fdcn_sm_extent", "fdcn_last_error", "fdcn_device_count",
+            "fdcn_abi_version")
+
+
+class FdcnError(RuntimeError):
+    pass
+
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+_PD = ctypes.POINTER(ctypes.c_double)
+_PI = ctypes.POINTER(ctypes.c_int32)
+_I = ctypes.c_int32
+_V = ctypes.c_void_p
+
+
+def lib() -> ctypes.CDLL:
+    """Load libfdcn.so (raises FdcnError if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise FdcnError(
+                    f"{LIB_PATH} is missing: build it with `python -c 'import "
+                    f"__graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+            L = ctypes.CDLL(LIB_PATH)
+            L.fdcn_cn_batch.restype = _I
+            L.fdcn_cn_batch.argtypes = [_I, _I, _I, _I, _PD, _PI, _PD, _I, _PI, _PD, _PD]
+            L.fdcn_it_batch.restype = _I
+            L.fdcn_it_batch.argtypes = [_I, _I, _I, _I, _PD, _PI, _PD, _PD, _PD]
+            L.fdcn_cn_batch_dev.restype = _I
+            L.fdcn_cn_batch_dev.argtypes = [_I, _I, _I, _I, _V, _V, _V, _I, _V, _V, _V, _I, _V,
+                                            _V]
+            L.fdcn_it_batch_dev.restype = _I
+            L.fdcn_it_batch_dev.argtypes = [_I, _I, _I, _I, _V, _V, _V, _V, _V, _I, _V, _V]
+            L.fdcn_plan.restype = _I
+            L.fdcn_plan.argtypes = [_I, _I, _I, _PI, _PI, _PI, _PI,
+                                    ctypes.POINTER(ctypes.c_int64)]
+            L.fdcn_sm_extent.restype = _I
+            L.fdcn_sm_extent.argtypes = [_I, _I, _I, _I, _PD]
+            L.fdcn_last_error.restype = ctypes.c_char_p
+            L.fdcn_last_error.argtypes = []
+            L.fdcn_device_count.restype = ctypes.c_int
+            L.fdcn_device_count.argtypes = []
+            L.fdcn_abi_version.restype = ctypes.c_int
+            L.fdcn_abi_version.argtypes = []
+            if L.fdcn_abi_version() != ABI_VERSION:
+                raise FdcnError("libfdcn.so ABI version mismatch; rebuild")
+            _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().fdcn_last_error().decode(errors="replace")
+        raise FdcnError(f"fdcn error {rc}: {msg}")
+
+
+def device_count() -> int:
+    return int(lib().fdcn_device_count())
+
+
+def require_device() -> None:
+    if device_count() < 1:
+        raise FdcnError("no gfx950 (MI355X) device visible; the CN engine has no CPU path")
+
+
+def _f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _i32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def plan(n_nodes: int, it_mode: bool, k_cap: int = 0) -> dict:
+    w, npt, spb, lds = (ctypes.c_int32() for _ in range(4))
+    ws = ctypes.c_int64()
+    _check(lib().fdcn_plan(n_nodes, 1 if it_mode else 0, k_cap, ctypes.byref(w),
+                           ctypes.byref(npt), ctypes.byref(spb), ctypes.byref(lds),
+                           ctypes.byref(ws)))
+    return dict(waves=w.value, npt=npt.value, scen_per_block=spb.value, lds_bytes=lds.value,
+                ws_bytes_per_scen=ws.value)
+
+
+def sm_extent(n_nodes: int, n_time: int, n_ranna: int, params: np.ndarray) -> int:
+    P = _f64(params).reshape(-1, NPARAM)
+    rc = lib().fdcn_sm_extent(P.shape[0], n_nodes, n_time, n_ranna, P.ctypes.data_as(_PD))
+    if rc < 0:
+        _check(rc)
+    return int(rc)
+
+
+def cn_batch(n_nodes: int, n_time: int, n_ranna: int, params, iparams, v_init, mon_step,
+             mon_rebate) -> np.ndarray:
+    """Host-array European/KO batch solve -> v_out [B, n_nodes]."""
+    require_device()
+    P, I, V = _f64(params), _i32(iparams), _f64(v_init)
+    B = V.shape[0]
+    ms = _i32(mon_step if len(mon_step) else [0])
+    mr = _f64(mon_rebate if len(mon_rebate) else [0.0])
+    out = np.empty((B, n_nodes), dtype=np.float64)
+    _check(lib().fdcn_cn_batch(B, n_nodes, n_time, n_ranna, P.ctypes.data_as(_PD),
+                               I.ctypes.data_as(_PI), V.ctypes.data_as(_PD), len(mon_step),
+                               ms.ctypes.data_as(_PI), mr.ctypes.data_as(_PD),
+                               out.ctypes.data_as(_PD)))
+    return out
+
+
+def it_batch(n_nodes: int, n_time: int, n_ranna: int, params, iparams, v_init,
+             payoff) -> np.ndarray:
+    """Host-array American (Ikonen-Toivanen) batch solve -> v_out [B, n_nodes]."""
+    require_device()
+    P, I, V, F = _f64(params), _i32(iparams), _f64(v_init), _f64(payoff)
+    B = V.shape[0]
+    out = np.empty((B, n_nodes), dtype=np.float64)
+    _check(lib().fdcn_it_batch(B, n_nodes, n_time, n_ranna, P.ctypes.data_as(_PD),
+                               I.ctypes.data_as(_PI), V.ctypes.data_as(_PD),
+                               F.ctypes.data_as(_PD), out.ctypes.data_as(_PD)))
+    return out
+
+
+def cn_batch_dev(B: int, n_nodes: int, n_time: int, n_ranna: int, params_ptr: int,
+                 iparams_ptr: int, v_init_ptr: int, n_mon: int, mon_step_ptr: int,
+                 mon_rebate_ptr: int, v_out_ptr: int, k_cap: int, workspace_ptr: int,
+                 stream_ptr: int) -> None:
+    """Device-pointer launch (asynchronous on `stream_ptr`)."""
+    _check(lib().fdcn_cn_batch_dev(B, n_nodes, n_time, n_ranna, params_ptr, iparams_ptr,
+                                   v_init_ptr, n_mon, mon_step_ptr, mon_rebate_ptr, v_out_ptr,
+                                   k_cap, workspace_ptr, stream_ptr))
+
+
+def it_batch_dev(B: int, n_nodes: int, n_time: int, n_ranna: int, params_ptr: int,
+                 iparams_ptr: int, v_init_ptr: int, payoff_ptr: int, v_out_ptr: int,
+                 k_cap: int, workspace_ptr: int, stream_ptr: int) -> None:
+    _check(lib().fdcn_it_batch_dev(B, n_nodes, n_time, n_ranna, params_ptr, iparams_ptr,
+                                   v_init_ptr, payoff_ptr, v_out_ptr, k_cap, workspace_ptr,
+                                   stream_ptr))

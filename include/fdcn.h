@@ -116,24 +116,30 @@ int fdcn_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
  * (v_out == v_init) only if `v_init` is not needed afterwards.
  * `k_cap` bounds the boundary-layer correction table (see fdcn_sm_extent);
  * pass the value fdcn_sm_extent returns for the same params.  A scenario whose
- * extent exceeds k_cap gets NaN outputs (loud, never silently wrong). */
+ * extent exceeds k_cap gets NaN outputs (loud, never silently wrong).
+ * `workspace` is device scratch of B * ws_bytes_per_scen bytes as reported by
+ * fdcn_plan for the same (n_nodes, mode, k_cap); NULL when that is 0 (the
+ * usual case: the correction table then lives in LDS). */
 int fdcn_cn_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                       const double* params, const int32_t* iparams,
                       const double* v_init,
                       int32_t n_mon, const int32_t* mon_step, const double* mon_rebate,
-                      double* v_out, int32_t k_cap, void* stream);
+                      double* v_out, int32_t k_cap, double* workspace, void* stream);
 
 int fdcn_it_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                       const double* params, const int32_t* iparams,
                       const double* v_init, const double* payoff,
-                      double* v_out, int32_t k_cap, void* stream);
+                      double* v_out, int32_t k_cap, double* workspace, void* stream);
 
 /* ---- launch planning / introspection ---------------------------------- */
 /* Writes the kernel geometry chosen for a launch: waves per scenario,
- * nodes per lane, scenarios per workgroup, LDS bytes per workgroup.
- * Returns FDCN_EINVAL if the size is unsupported. */
+ * nodes per lane, scenarios per workgroup, LDS bytes per workgroup, and the
+ * device workspace the _dev entry points need per scenario (0 = none).
+ * Any output pointer may be NULL.  Returns FDCN_EINVAL if the size is
+ * unsupported. */
 int fdcn_plan(int32_t n_nodes, int32_t it_mode, int32_t k_cap, int32_t* waves,
-              int32_t* npt, int32_t* scen_per_block, int32_t* lds_bytes);
+              int32_t* npt, int32_t* scen_per_block, int32_t* lds_bytes,
+              int64_t* ws_bytes_per_scen);
 
 /* Extent (nodes) of the Sherman-Morrison boundary-layer correction needed by
  * the scenarios in `params` (host memory): the largest k such that the

@@ -14,7 +14,7 @@
  *     operand order, and the file is compiled with -ffp-contract=off, so the
  *     results are bit-identical to the Python reference (CPython floats are
  *     IEEE binary64, math.exp is libm exp).  tests/test_oracle_golden.py
- *     checks that bit-for-bit against tests/golden/*.json.
+ *     checks that bit-for-bit against the JSON vectors in tests/golden.
  *
  *  2. oracle_cn_batch / oracle_it_batch: the same algorithm driven by the
  *     C-ABI's plan arrays (include/fdcn.h), so a plan built by the product's
