@@ -1,0 +1,651 @@
+"""Discrete-barrier pricer: CN + Rannacher in log-spot with knock-out
+projection on monitoring steps; knock-ins by in/out parity with Black-76.
+
+Drop-in for ``DiscreteBarrierFDMPricer`` (discrete_barrier_fdm_pricer.py:33-
+1084, the executable part of the file).  Constructor keywords, public methods
+(``price_log2``, ``greeks_log2``, ``print_details``) and numerics follow the
+reference, including the behaviours the committed golden results depend on:
+
+* ``num_space_nodes`` is replaced by ceil(norm.ppf(0.99999) * N_time)
+  (choose_grid_parameters, :270-320);
+* the solve drops the top grid node on its first step (:449, :543): the march
+  runs on nodes 0..N_s-1 with the Dirichlet value of the true top node;
+* the put's lower boundary is K e^{-r tau} S_min e^{(b-r) tau} (:391);
+* monitoring step k = max(1, min(N_t, floor((T - t)/dt + 1e-9))) (:395-411).
+
+What changes is the execution: ``_pde_price_and_greeks3`` needs a base and a
+sigma-bumped solve, and price_log2 + greeks_log2 ask for that pair twice; the
+pair is marched as one two-scenario launch on the MI355X and cached, and
+``price_many`` batches every trade of a scenario file into one launch per
+grid shape.
+"""
+from __future__ import annotations
+
+import bisect
+import datetime as _dt
+import math
+from typing import Any, Dict, List, Literal, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import market
+from .engine import (FORM_PROD, FORM_SUM, Boundary, Engine, Solve, default_engine,
+                     operator_coefficients)
+
+BarrierType = Literal["down-and-out", "up-and-out", "double-out", "down-and-in", "up-and-in",
+                      "double-in", "none"]
+OptionType = Literal["call", "put"]
+
+KO_TYPES = ("down-and-out", "up-and-out", "double-out")
+KI_TO_KO = {"down-and-in": "down-and-out", "up-and-in": "up-and-out",
+            "double-in": "double-out"}
+
+
+def _ppf_99999() -> float:
+    from scipy.stats import norm
+    return float(norm.ppf(0.99999))
+
+
+_K_TAIL: Optional[float] = None
+
+
+def tail_quantile() -> float:
+    """norm.ppf(0.99999), the half-width factor of the log-spot domain."""
+    global _K_TAIL
+    if _K_TAIL is None:
+        _K_TAIL = _ppf_99999()
+    return _K_TAIL
+
+
+def _norm_cdf(x: float) -> float:
+    from scipy.stats import norm
+    return float(norm.cdf(x))
+
+
+class _Grid:
+    __slots__ = ("n_space", "n_time", "S_min", "S_max", "dx", "s_nodes")
+
+    def __init__(self, n_space, n_time, S_min, S_max, dx, s_nodes):
+        self.n_space, self.n_time = n_space, n_time
+        self.S_min, self.S_max, self.dx, self.s_nodes = S_min, S_max, dx, s_nodes
+
+
+class DiscreteBarrierFDMPricer:
+    """CN FDM pricer for discretely monitored European barrier options."""
+
+    def __init__(
+        self,
+        spot: float,
+        strike: float,
+        valuation_date: _dt.date,
+        maturity_date: _dt.date,
+        sigma: float,
+        option_type: OptionType,
+        barrier_type: BarrierType = "none",
+        lower_barrier: Optional[float] = None,
+        upper_barrier: Optional[float] = None,
+        monitor_dates: Optional[List[_dt.date]] = None,
+        rebate_amount: float = 0.0,
+        rebate_at_hit: bool = False,
+        already_hit: bool = False,
+        already_in: bool = False,
+        underlying_spot_days: float = 3,
+        option_days: float = 0,
+        option_settlement_days: float = 0,
+        discount_curve: Optional[Any] = None,
+        forward_curve: Optional[Any] = None,
+        dividend_schedule: Optional[List[Tuple[_dt.date, float]]] = None,
+        trade_id: float = None,
+        direction: Literal["long", "short"] = "long",
+        quantity: int = 1,
+        contract_multiplier: float = 1.0,
+        min_substeps_between_monitors: int = 1,
+        grid_type: Literal["uniform", "sinh"] = "uniform",
+        sinh_alpha: float = 1.5,
+        lambda_diff_target: float = 0.5,
+        num_space_nodes: int = 400,
+        num_time_steps: int = 400,
+        rannacher_steps: int = 2,
+        s_max_mult: float = 4.5,
+        restart_on_monitoring: bool = False,
+        use_one_sided_greeks_near_barrier: bool = True,
+        mollify_final: bool = True,
+        mollify_band_nodes: int = 2,
+        price_extrapolation: bool = False,
+        day_count: str = "ACT/365",
+        calculate_greeks_in_pde: bool = True,
+        engine: Optional[Engine] = None,
+    ) -> None:
+        if any(x <= 0 for x in (spot, strike, sigma)):
+            raise ValueError("spot, strike, sigma must be positive.")
+        if maturity_date <= valuation_date:
+            raise ValueError("maturity_date must be after valuation_date.")
+        self.spot = spot
+        self.strike = strike
+        self.valuation_date = valuation_date
+        self.maturity_date = maturity_date
+        self.sigma = sigma
+        self.option_type = option_type
+        self.barrier_type = barrier_type
+        self.lower_barrier = lower_barrier
+        self.upper_barrier = upper_barrier
+        self.monitor_dates = sorted(monitor_dates or [])
+        self.rebate_amount = rebate_amount
+        self.rebate_at_hit = rebate_at_hit
+        self.already_hit = already_hit
+        self.already_in = already_in
+        self.underlying_spot_days = underlying_spot_days
+        self.option_days = option_days
+        self.option_settlement_days = option_settlement_days
+        self.calendar = market.SouthAfrica()
+
+        self.discount_curve_df = discount_curve.copy() if discount_curve is not None else None
+        self.forward_curve_df = forward_curve.copy() if forward_curve is not None else None
+        self._curve = (market.NacaCurve(self.discount_curve_df)
+                       if self.discount_curve_df is not None else None)
+        self.dividend_schedule = sorted(dividend_schedule or [], key=lambda x: x[0])
+
+        self.trade_id = trade_id
+        self.direction = direction
+        self.quantity = int(quantity)
+        self.contract_multiplier = float(contract_multiplier)
+
+        self.num_space_nodes = int(num_space_nodes)
+        self.num_time_steps = int(num_time_steps)
+        self.rannacher_steps = int(rannacher_steps)
+        self.min_substeps = max(1, int(min_substeps_between_monitors))
+        self.lambda_diff_target = float(lambda_diff_target)
+        self.s_max_mult = s_max_mult
+        self.restart_on_monitoring = restart_on_monitoring
+        self.mollify_final = mollify_final
+        self.mollify_band_nodes = int(mollify_band_nodes)
+        self.price_extrapolation = price_extrapolation
+        self.use_one_sided_greeks_near_barrier = use_one_sided_greeks_near_barrier
+        self.calculate_greeks_in_pde = calculate_greeks_in_pde
+
+        self.day_count = market.normalise_day_count(day_count)
+        self._year_denominator = market.year_denominator(self.day_count)
+
+        cal = self.calendar
+        self.carry_start_date = cal.add_working_days(valuation_date, underlying_spot_days)
+        self.carry_end_date = cal.add_working_days(maturity_date, underlying_spot_days)
+        self.discount_start_date = cal.add_working_days(valuation_date, option_days)
+        self.discount_end_date = cal.add_working_days(maturity_date, option_settlement_days)
+
+        self.time_to_expiry = self._year_fraction(valuation_date, maturity_date)
+        self.time_to_carry = self._year_fraction(self.carry_start_date, self.carry_end_date)
+        self.time_to_discount = self._year_fraction(self.discount_start_date,
+                                                    self.discount_end_date)
+
+        self.discount_rate_nacc = self.get_forward_nacc_rate(self.discount_start_date,
+                                                             self.discount_end_date)
+        self.carry_rate_nacc = self.get_forward_nacc_rate(self.carry_start_date,
+                                                          self.carry_end_date)
+        self.div_yield_nacc = self.dividend_yield_nacc()
+        self.pv_divs = self.pv_dividends()
+        self.forward_price = self.spot * math.exp((self.carry_rate_nacc - self.div_yield_nacc)
+                                                  * self.time_to_carry)
+        self.b = math.log(self.forward_price / self.spot) / self.time_to_carry
+
+        self.grid_type = grid_type
+        self.sinh_alpha = sinh_alpha
+        self.time_spacing = self.time_to_expiry / self.num_time_steps
+        self.time_grid = [i * self.time_to_expiry / self.num_time_steps
+                          for i in range(self.num_time_steps + 1)]
+        self.monitor_times = self._build_monitor_times_exact()
+
+        self.s_nodes: List[float] = []
+        self._S_min = 0.0
+        self._S_max = 0.0
+        self.engine = engine
+        self._pde_cache: Dict[tuple, Dict[str, float]] = {}
+
+    # ------------------------------------------------------------- calendar
+    def _infer_denominator(self, day_count: str) -> int:
+        return market.year_denominator(day_count)
+
+    def _year_fraction(self, start_date: _dt.date, end_date: _dt.date) -> float:
+        return market.year_fraction(self.day_count, start_date, end_date)
+
+    def get_discount_factor(self, lookup_date: _dt.date) -> float:
+        if self._curve is None:
+            raise ValueError("No discount curve attached.")
+        return market.discount_factor(self._curve, self.day_count, self.valuation_date,
+                                      lookup_date)
+
+    def get_nacc_rate(self, lookup_date: _dt.date) -> float:
+        if self._curve is None:
+            return 0.0
+        naca = self._curve.naca(lookup_date)
+        return 0.0 if naca is None else math.log(1.0 + naca)
+
+    def get_forward_nacc_rate(self, start_date: _dt.date, end_date: _dt.date) -> float:
+        df_far = self.get_discount_factor(end_date)
+        df_near = self.get_discount_factor(start_date)
+        tau = self._year_fraction(start_date, end_date)
+        return -math.log(df_far / df_near) / max(1e-12, tau)
+
+    def pv_dividends(self) -> float:
+        """PV at valuation of cash dividends in (valuation, maturity] (:232-242)."""
+        pv = 0.0
+        for pay_date, amount in self.dividend_schedule:
+            if self.valuation_date < pay_date <= self.maturity_date:
+                df = (self.get_discount_factor(pay_date)
+                      / self.get_discount_factor(self.carry_start_date))
+                pv += amount * df
+        return pv
+
+    def dividend_yield_nacc(self) -> float:
+        """Flat q reproducing PV(dividends) over the carry window (:244-255)."""
+        pv = self.pv_dividends()
+        S = self.spot
+        tau = max(1e-12, self.time_to_carry)
+        if pv <= 0.0:
+            return 0.0
+        if pv >= S:
+            raise ValueError("PV(dividend_schedule) >= spot.")
+        return -math.log((S - pv) / S) / tau
+
+    def _build_monitor_times_exact(self) -> List[float]:
+        """Monitoring year fractions in [0, T], T appended (:257-268).
+
+        The reference indexes times[-1] and raises IndexError on an empty
+        list; here an empty list means "monitor at maturity only"."""
+        times = []
+        for d in self.monitor_dates:
+            if self.valuation_date <= d <= self.maturity_date:
+                t = self._year_fraction(self.valuation_date, d)
+                if 0.0 <= t <= self.time_to_expiry:
+                    times.append(t)
+        if not times or times[-1] < self.time_to_expiry - 1e-14:
+            times.append(self.time_to_expiry)
+        return sorted(set(times))
+
+    # ------------------------------------------------------------------ grid
+    def choose_grid_parameters(self, S0: float, K: float, lower_barrier: Optional[float],
+                               upper_barrier: Optional[float], T: float,
+                               sigma: float) -> Tuple[int, int, float, float]:
+        """(N_space, N_time, S_min, S_max); N_space derived from N_time (:270-320)."""
+        if T <= 0.0:
+            raise ValueError("Maturity T must be positive.")
+        if sigma <= 0.0:
+            raise ValueError("Volatility sigma must be positive.")
+        if S0 <= 0.0:
+            raise ValueError("Spot S0 must be positive.")
+        cands = [S0, K]
+        if lower_barrier is not None and lower_barrier > 0.0:
+            cands.append(lower_barrier)
+        if upper_barrier is not None and upper_barrier > 0.0:
+            cands.append(upper_barrier)
+        s_low, s_high = min(cands), max(cands)
+        k = tail_quantile()
+        width = 2.0 * k * sigma * math.sqrt(self.time_to_expiry)
+        x_c = math.log(math.sqrt(s_low * s_high))
+        S_min = min(math.exp(x_c - 0.5 * width), 0.5 * s_low)
+        S_max = max(math.exp(x_c + 0.5 * width), 2 * s_high)
+        N_time = self.num_time_steps
+        N_space = math.ceil((width * N_time) / (2 * sigma * math.sqrt(self.time_to_expiry)))
+        return N_space, N_time, S_min, S_max
+
+    def configure_grid(self) -> None:
+        N_space, N_time, S_min, S_max = self.choose_grid_parameters(
+            S0=self.spot - self.pv_divs, K=self.strike, lower_barrier=self.lower_barrier,
+            upper_barrier=self.upper_barrier, T=self.time_to_expiry, sigma=self.sigma)
+        self.num_space_nodes = N_space
+        self.num_time_steps = N_time
+        self._S_min = S_min
+        self._S_max = S_max
+
+    def _grid(self) -> _Grid:
+        self.configure_grid()
+        x_min, x_max = math.log(self._S_min), math.log(self._S_max)
+        n = self.num_space_nodes
+        dx = (x_max - x_min) / n
+        s = list(map(math.exp, [x_min + i * dx for i in range(n + 1)]))
+        return _Grid(n, self.num_time_steps, self._S_min, self._S_max, dx, s)
+
+    def _build_log_grid(self) -> float:
+        g = self._grid()
+        self.s_nodes = g.s_nodes
+        self.lower_barrier_log = math.log(self.lower_barrier) if self.lower_barrier else None
+        self.upper_barrier_log = math.log(self.upper_barrier) if self.upper_barrier else None
+        return g.dx
+
+    def _terminal_payoff(self) -> List[float]:
+        return self._payoff(self.s_nodes).tolist()
+
+    def _payoff(self, s_nodes) -> np.ndarray:
+        s = np.asarray(s_nodes, dtype=np.float64)
+        e = s - self.strike if self.option_type == "call" else self.strike - s
+        return np.where(0.0 > e, 0.0, e)  # Python max(e, 0.0)
+
+    def _boundary_values(self, tau: float) -> Tuple[float, float]:
+        lo, hi = self._boundaries(self.s_nodes)
+        return lo.value(tau), hi.value(tau)
+
+    def _boundaries(self, s_nodes) -> Tuple[Boundary, Boundary]:
+        """Dirichlet values of :372-393 (put lower value keeps the S_min factor)."""
+        r, b, k = self.discount_rate_nacc, self.carry_rate_nacc, self.strike
+        if self.option_type.lower() == "call":
+            return Boundary(), Boundary(FORM_SUM, s_nodes[-1], b - r, -k, -r)
+        return Boundary(FORM_PROD, k, -r, s_nodes[0], b - r), Boundary()
+
+    def _monitor_indices_tau(self, dt: float) -> set:
+        idx = set()
+        for t_mon in self.monitor_times:
+            if t_mon <= 0.0 or t_mon > self.time_to_expiry:
+                continue
+            k = int(math.floor((self.time_to_expiry - t_mon) / dt + 1e-9))
+            idx.add(max(1, min(self.num_time_steps, k)))
+        return idx
+
+    def _ko_thresholds(self, s_nodes: Sequence[float], n_nodes: int,
+                       barrier_type: str) -> Tuple[int, int]:
+        """Integer node thresholds equivalent to the per-node compares of
+        _apply_KO_projection (:413-440) over nodes 0..n_nodes-1."""
+        ko_lo, ko_hi = -1, n_nodes
+        lo, up = self.lower_barrier, self.upper_barrier
+        s = list(s_nodes[:n_nodes])
+        if barrier_type in ("down-and-out", "double-out") and lo is not None:
+            ko_lo = bisect.bisect_right(s, lo) - 1      # last j with s_j <= lo
+        if barrier_type in ("up-and-out", "double-out") and up is not None:
+            ko_hi = bisect.bisect_left(s, up)           # first j with s_j >= up
+        return ko_lo, ko_hi
+
+    def _apply_KO_projection(self, V: List[float], s_nodes: List[float], tau_left: float) -> None:
+        """Host version of the projection (the kernel applies it in-launch)."""
+        if self.barrier_type in ("none", "down-and-in", "up-and-in", "double-in"):
+            return
+        reb = self._rebate(tau_left)
+        n = min(len(V), len(s_nodes))
+        ko_lo, ko_hi = self._ko_thresholds(s_nodes, n, self.barrier_type)
+        for i in range(n):
+            if i <= ko_lo or i >= ko_hi:
+                V[i] = reb
+
+    def _rebate(self, tau: float) -> float:
+        if self.rebate_at_hit:
+            return self.rebate_amount
+        return self.rebate_amount * math.exp(-self.carry_rate_nacc * tau)
+
+    # ----------------------------------------------------------------- solve
+    def _engine(self) -> Engine:
+        return self.engine if self.engine is not None else default_engine()
+
+    def _make_solve(self, apply_KO: bool, sigma: float,
+                    N_time: Optional[int] = None) -> Tuple[Solve, _Grid]:
+        """The work of one _solve_grid call (:442-547) as a kernel scenario."""
+        sig0 = self.sigma
+        self.sigma = sigma
+        try:
+            g = self._grid()
+        finally:
+            self.sigma = sig0
+        n_steps = int(N_time) if N_time is not None else int(self.num_time_steps)
+        dt = self.time_to_expiry / self.num_time_steps
+        coeffs = operator_coefficients(sigma, self.carry_rate_nacc, self.div_yield_nacc,
+                                       self.discount_rate_nacc, g.dx)
+        n_nodes = g.n_space  # top node dropped on the first step (:449, :543)
+        v0 = self._payoff(g.s_nodes)[:n_nodes]
+        lower, upper = self._boundaries(g.s_nodes)
+        solve = Solve(it=False, n_time=n_steps, n_ranna=min(self.rannacher_steps, n_steps),
+                      dt=dt, coeffs=coeffs, v_init=v0, lower=lower, upper=upper)
+        if apply_KO and self.barrier_type in KO_TYPES:
+            solve.ko_lo, solve.ko_hi = self._ko_thresholds(g.s_nodes, n_nodes,
+                                                           self.barrier_type)
+            steps = sorted(k for k in self._monitor_indices_tau(dt) if 1 <= k <= n_steps)
+            solve.mon_steps = steps
+            solve.mon_rebates = [self._rebate(k * dt) for k in steps]
+        return solve, g
+
+    def _solve_grid(self, apply_KO: bool, N_time: int = None) -> List[float]:
+        """Value vector at valuation on nodes 0..N_s-1 (the reference's list)."""
+        solve, g = self._make_solve(apply_KO, self.sigma, N_time)
+        self.s_nodes = g.s_nodes
+        return self._engine().run([solve])[0].tolist()
+
+    # ------------------------------------------------------- grid epilogue
+    def _interp_price(self, V: Sequence[float], s_nodes: Optional[Sequence[float]] = None) -> float:
+        s = self.s_nodes if s_nodes is None else s_nodes
+        S0 = self.spot - self.pv_divs
+        if S0 <= s[0]:
+            return float(V[0])
+        if S0 >= s[-1]:
+            return float(V[-1])
+        hi = bisect.bisect_right(s, S0)
+        lo = hi - 1
+        w = (S0 - s[lo]) / (s[hi] - s[lo])
+        return float((1.0 - w) * V[lo] + w * V[hi])
+
+    def _delta_gamma_from_grid(self, V: Sequence[float],
+                               s_nodes: Optional[Sequence[float]] = None) -> Tuple[float, float]:
+        """Non-uniform 3-point stencil at the interior node nearest spot (:949-978)."""
+        s = self.s_nodes if s_nodes is None else s_nodes
+        S0 = self.spot
+        sa = np.asarray(s[1:len(s) - 1])
+        idx = 1 + int(np.argmin(np.abs(sa - S0)))
+        h1 = s[idx] - s[idx - 1]
+        h2 = s[idx + 1] - s[idx]
+        Vm, V0, Vp = V[idx - 1], V[idx], V[idx + 1]
+        delta = (-h2 / (h1 * (h1 + h2)) * Vm + (h2 - h1) / (h1 * h2) * V0
+                 + h1 / (h2 * (h1 + h2)) * Vp)
+        gamma = 2.0 * (Vm / (h1 * (h1 + h2)) - V0 / (h1 * h2) + Vp / (h2 * (h1 + h2)))
+        return delta, gamma
+
+    def _map_KI_to_KO(self) -> Optional[str]:
+        return KI_TO_KO.get(self.barrier_type)
+
+    # ------------------------------------------------------------- vanilla
+    def _vanilla_black76_price(self, S: Optional[float] = None, sigma: Optional[float] = None,
+                               T: Optional[float] = None) -> float:
+        """Black-76 on the dividend-adjusted forward (:648-692)."""
+        S = self.spot - self.pv_divs if S is None else S - self.pv_divs
+        K = self.strike
+        t_exp = self.time_to_expiry if T is None else T
+        sigma = self.sigma if sigma is None else sigma
+        if self.time_to_discount <= 0 or sigma <= 0:
+            return max(S - K, 0.0) if self.option_type == "call" else max(K - S, 0.0)
+        sqrtT = math.sqrt(t_exp)
+        F = S * math.exp(self.carry_rate_nacc * self.time_to_carry)
+        d1 = (math.log(F / K) + (0.5 * sigma * sigma) * t_exp) / (sigma * sqrtT)
+        d2 = d1 - sigma * sqrtT
+        Nd1, Nd2 = _norm_cdf(d1), _norm_cdf(d2)
+        disc = math.exp(-self.discount_rate_nacc * self.time_to_discount)
+        if self.option_type == "call":
+            return disc * (F * Nd1 - K * Nd2)
+        return disc * (K * (1.0 - Nd2) - F * (1.0 - Nd1))
+
+    def _vanilla_black76_greeks_fd(self, dS: float = 0.0001, dSigma: float = 0.0001,
+                                   dT: float = 0.0001) -> Dict[str, float]:
+        """Bump-and-revalue Greeks of the Black-76 price (:694-745)."""
+        S0, sig0, T0 = self.spot, self.sigma, self.time_to_expiry
+        h = S0 * dS
+        p0 = self._vanilla_black76_price(S=S0, sigma=sig0, T=T0)
+        pu = self._vanilla_black76_price(S=S0 + h, sigma=sig0, T=T0)
+        pd_ = self._vanilla_black76_price(S=S0 - h, sigma=sig0, T=T0)
+        delta = (pu - pd_) / (2.0 * h)
+        gamma = (pu - 2.0 * p0 + pd_) / (h ** 2)
+        vega = (self._vanilla_black76_price(S=S0, sigma=sig0 + dSigma, T=T0) - p0) / (100 * dSigma)
+        if T0 > 2.0 * dT:
+            theta = -((self._vanilla_black76_price(S=S0, sigma=sig0, T=T0 + dT)
+                       - self._vanilla_black76_price(S=S0, sigma=sig0, T=T0 - dT)) / (2.0 * dT))
+        else:
+            theta = -((p0 - self._vanilla_black76_price(S=S0, sigma=sig0,
+                                                         T=max(T0 - dT, 1e-8))) / dT)
+        return {"price": p0, "delta": delta, "gamma": gamma, "theta": theta, "vega": vega}
+
+    # ------------------------------------------------------------ PDE greeks
+    def _pde_key(self, apply_KO: bool, dv_sigma: float) -> tuple:
+        return (apply_KO, float(dv_sigma), self.barrier_type, self.option_type, self.spot,
+                self.strike, self.sigma, self.lower_barrier, self.upper_barrier,
+                self.rebate_amount, self.rebate_at_hit, self.num_time_steps,
+                self.rannacher_steps, self.time_to_expiry, self.discount_rate_nacc,
+                self.carry_rate_nacc, self.div_yield_nacc, self.pv_divs,
+                tuple(self.monitor_times))
+
+    def pde_solves(self, apply_KO: bool = True, dv_sigma: float = 0.0001):
+        """The base and sigma-bumped solves _pde_price_and_greeks3 needs."""
+        base = self._make_solve(apply_KO, self.sigma)
+        bump = self._make_solve(apply_KO, self.sigma + dv_sigma)
+        return base, bump
+
+    def _pde_finish(self, Vb: np.ndarray, gb: _Grid, Vu: np.ndarray, gu: _Grid,
+                    dv_sigma: float) -> Dict[str, float]:
+        price_base = self._interp_price(Vb, gb.s_nodes)
+        delta, gamma = self._delta_gamma_from_grid(Vb, gb.s_nodes)
+        price_up = self._interp_price(Vu, gu.s_nodes)
+        vega = (price_up - price_base) / (dv_sigma * 100)
+        theta = -(0.5 * self.sigma * self.sigma * self.spot * self.spot * gamma
+                  + (self.carry_rate_nacc - self.div_yield_nacc) * self.spot * delta
+                  - self.discount_rate_nacc * price_base)
+        return {"price": price_base, "delta": delta, "gamma": gamma, "vega": vega,
+                "theta": theta}
+
+    def _pde_price_and_greeks3(self, apply_KO: bool, dv_sigma: float = 0.0001,
+                               use_richardson: bool = False) -> Dict[str, float]:
+        """Base + bumped solve in one launch; cached (:883-904)."""
+        key = self._pde_key(apply_KO, dv_sigma)
+        hit = self._pde_cache.get(key)
+        if hit is None:
+            (sb, gb), (su, gu) = self.pde_solves(apply_KO, dv_sigma)
+            Vb, Vu = self._engine().run([sb, su])
+            hit = self._pde_finish(Vb, gb, Vu, gu, dv_sigma)
+            self._pde_cache[key] = hit
+            self.s_nodes = gu.s_nodes  # the reference leaves the bumped grid behind
+            self.num_space_nodes = gu.n_space
+        return dict(hit)
+
+    # ---------------------------------------------------------------- public
+    def price_log2(self, apply_KO: bool = True, use_richardson: bool = False) -> float:
+        """Vanilla: Black-76; KO: PDE; KI: vanilla - KO (:907-946)."""
+        bt = self.barrier_type.lower()
+        if bt == "none":
+            return self._vanilla_black76_price()
+        if bt in ("down-and-out", "up-and-out"):
+            if self.already_hit:
+                return self.rebate_amount * self.get_discount_factor(self.discount_end_date)
+            return self._pde_price_and_greeks3(True, 0.0001, use_richardson)["price"]
+        if bt in ("down-and-in", "up-and-in"):
+            if self.already_in:
+                return self._vanilla_black76_price()
+            p_van = self._vanilla_black76_price()
+            self.barrier_type = KI_TO_KO[bt]
+            try:
+                g_ko = self._pde_price_and_greeks3(True, 0.0001, use_richardson)
+            finally:
+                self.barrier_type = bt
+            return p_van - g_ko["price"]
+        raise ValueError(f"Unsupported barrier_type: {self.barrier_type}")
+
+    def greeks_log2(self, dv_sigma: float = 0.0001, use_richardson: bool = False) -> Dict[str, float]:
+        """Greeks consistent with price_log2 (:980-1026)."""
+        bt = self.barrier_type.lower()
+        if bt == "none":
+            return self._vanilla_black76_greeks_fd()
+        if bt in ("down-and-out", "up-and-out"):
+            if self.already_hit:
+                return {"price": 0.00, "delta": 0.00, "gamma": 0.00, "vega": 0.00,
+                        "theta": 0.00}
+            return self._pde_price_and_greeks3(True, dv_sigma, use_richardson)
+        if bt in ("down-and-in", "up-and-in"):
+            if self.already_in:
+                return self._vanilla_black76_greeks_fd()
+            self.barrier_type = "none"
+            g_van = self._vanilla_black76_greeks_fd()
+            self.barrier_type = KI_TO_KO[bt]
+            try:
+                g_ko = self._pde_price_and_greeks3(True, dv_sigma, use_richardson)
+            finally:
+                self.barrier_type = bt
+            return {k: g_van[k] - g_ko[k] for k in g_van.keys()}
+        raise ValueError(f"Unsupported barrier_type: {self.barrier_type}")
+
+    def print_details(self) -> None:
+        p = self.price_log2()
+        g = self.greeks_log2()
+        self._build_log_grid()
+        print("==== Discrete Barrier Option (CN + Rannacher) — Discrete monitors, no BGK ====")
+        print(f"T (years)         : {self.time_to_expiry:.9f}   [{self.day_count}]")
+        print(f"sigma / r / q     : {self.sigma:.9f} / {self.carry_rate_nacc:.9f} / "
+              f"{self.div_yield_nacc:.9f}")
+        print(f"Barrier type      : {self.barrier_type}  (lo={self.lower_barrier}, "
+              f"up={self.upper_barrier})")
+        print(f"Rebate (amt/hit)  : {self.rebate_amount} / {self.rebate_at_hit}")
+        print(f"Status (hit/in)   : {self.already_hit} / {self.already_in}")
+        print(f"Grid(S,N)         : {len(self.s_nodes)}, {self.num_time_steps}  | "
+              f"grid_type={self.grid_type}")
+        print(f"Monitors (count)  : {len(self.monitor_times)} @ {self.monitor_times}")
+        print(f"Spot/Strike       : {self.spot:.6f} / {self.strike:.6f}")
+        print(f"Price             : {p:.9f}")
+        print(f"Greeks            : Δ={g['delta']:.9f}, Γ={g['gamma']:.9f}, "
+              f"ν={g['vega']:.9f}, Θ={g['theta']:.9f}")
+
+    def validate_convergence(self, N_list: List[int], M_list: List[int]) -> List[Dict[str, float]]:
+        """Price and Greeks over (N, M) grids.  The reference calls the
+        non-existent price_log/greeks_log (:1066-1067); this uses the *_log2
+        pair, batched over all grids."""
+        clones = []
+        for N in N_list:
+            for M in M_list:
+                clones.append((N, M, DiscreteBarrierFDMPricer(
+                    spot=self.spot, strike=self.strike, valuation_date=self.valuation_date,
+                    maturity_date=self.maturity_date, sigma=self.sigma,
+                    discount_curve=self.discount_curve_df, forward_curve=self.forward_curve_df,
+                    dividend_schedule=self.dividend_schedule, option_type=self.option_type,
+                    barrier_type=self.barrier_type, lower_barrier=self.lower_barrier,
+                    upper_barrier=self.upper_barrier, monitor_dates=self.monitor_dates,
+                    rebate_amount=self.rebate_amount, rebate_at_hit=self.rebate_at_hit,
+                    already_hit=self.already_hit, already_in=self.already_in,
+                    num_space_nodes=N, num_time_steps=M, rannacher_steps=self.rannacher_steps,
+                    day_count=self.day_count, underlying_spot_days=self.underlying_spot_days,
+                    option_days=self.option_days,
+                    option_settlement_days=self.option_settlement_days,
+                    min_substeps_between_monitors=self.min_substeps, grid_type=self.grid_type,
+                    sinh_alpha=self.sinh_alpha,
+                    use_one_sided_greeks_near_barrier=self.use_one_sided_greeks_near_barrier,
+                    mollify_band_nodes=self.mollify_band_nodes, engine=self.engine)))
+        price_many([c for _, _, c in clones])
+        out = []
+        for N, M, c in clones:
+            g = c.greeks_log2()
+            out.append({"N": N, "M": M, "price": c.price_log2(), "delta": g["delta"],
+                        "gamma": g["gamma"], "vega": g["vega"], "theta": g["theta"]})
+        out.sort(key=lambda r: (r["N"], r["M"]))
+        return out
+
+
+def price_many(pricers: Sequence[DiscreteBarrierFDMPricer], dv_sigma: float = 0.0001) -> None:
+    """Run the PDE solves of many trades together (one launch per grid shape)
+    and fill each pricer's cache, so price_log2 / greeks_log2 return at once."""
+    todo = []
+    solves: List[Solve] = []
+    for p in pricers:
+        bt = p.barrier_type.lower()
+        if bt in ("down-and-out", "up-and-out") and not p.already_hit:
+            kbt = bt
+        elif bt in ("down-and-in", "up-and-in") and not p.already_in:
+            kbt = KI_TO_KO[bt]
+        else:
+            continue
+        keep = p.barrier_type
+        p.barrier_type = kbt
+        try:
+            key = p._pde_key(True, dv_sigma)
+            if key in p._pde_cache:
+                continue
+            (sb, gb), (su, gu) = p.pde_solves(True, dv_sigma)
+        finally:
+            p.barrier_type = keep
+        todo.append((p, kbt, key, gb, gu))
+        solves.extend([sb, su])
+    if not solves:
+        return
+    engine = pricers[0]._engine()
+    res = engine.run(solves)
+    for i, (p, kbt, key, gb, gu) in enumerate(todo):
+        keep = p.barrier_type
+        p.barrier_type = kbt
+        try:
+            p._pde_cache[key] = p._pde_finish(res[2 * i], gb, res[2 * i + 1], gu, dv_sigma)
+        finally:
+            p.barrier_type = keep
