@@ -115,6 +115,7 @@ class DiscreteBarrierFDMPricer:
         day_count: str = "ACT/365",
         calculate_greeks_in_pde: bool = True,
         engine: Optional[Engine] = None,
+        grid_mode: Literal["parity", "explicit"] = "parity",
     ) -> None:
         if any(x <= 0 for x in (spot, strike, sigma)):
             raise ValueError("spot, strike, sigma must be positive.")
@@ -198,6 +199,13 @@ class DiscreteBarrierFDMPricer:
         self._S_min = 0.0
         self._S_max = 0.0
         self.engine = engine
+        if grid_mode not in ("parity", "explicit"):
+            raise ValueError("grid_mode must be 'parity' or 'explicit'")
+        # "parity": N_space = ceil(norm.ppf(0.99999) N_time), as the reference
+        # (choose_grid_parameters :317).  "explicit": N_space = num_space_nodes
+        # as requested (BASELINE config 3's 1024 x 2000 grids).
+        self.grid_mode = grid_mode
+        self._requested_space_nodes = int(num_space_nodes)
         self._pde_cache: Dict[tuple, Dict[str, float]] = {}
 
     # ------------------------------------------------------------- calendar
@@ -284,6 +292,8 @@ class DiscreteBarrierFDMPricer:
         S_min = min(math.exp(x_c - 0.5 * width), 0.5 * s_low)
         S_max = max(math.exp(x_c + 0.5 * width), 2 * s_high)
         N_time = self.num_time_steps
+        if getattr(self, "grid_mode", "parity") == "explicit":
+            return self._requested_space_nodes, N_time, S_min, S_max
         N_space = math.ceil((width * N_time) / (2 * sigma * math.sqrt(self.time_to_expiry)))
         return N_space, N_time, S_min, S_max
 
@@ -476,7 +486,8 @@ class DiscreteBarrierFDMPricer:
 
     # ------------------------------------------------------------ PDE greeks
     def _pde_key(self, apply_KO: bool, dv_sigma: float) -> tuple:
-        return (apply_KO, float(dv_sigma), self.barrier_type, self.option_type, self.spot,
+        return (apply_KO, float(dv_sigma), self.grid_mode, self._requested_space_nodes,
+                self.barrier_type, self.option_type, self.spot,
                 self.strike, self.sigma, self.lower_barrier, self.upper_barrier,
                 self.rebate_amount, self.rebate_at_hit, self.num_time_steps,
                 self.rannacher_steps, self.time_to_expiry, self.discount_rate_nacc,

@@ -77,7 +77,7 @@ def make_barrier_pricer(S0, K, sigma, rate, barrier_type, upper_barrier, lower_b
                         underlying_spot_days: int = 0, option_days: int = 0,
                         option_settlement_days: int = 0, day_count: str = "ACT/365",
                         grid_type: str = "uniform", num_space_nodes: int = 500,
-                        num_time_steps: int = 500,
+                        num_time_steps: int = 500, grid_mode: str = "parity",
                         engine: Optional[Engine] = None) -> DiscreteBarrierFDMPricer:
     """The pricer run_scenario builds (run_config_scenarios.py:60-94)."""
     curve = _flat_curve(rate)
@@ -93,7 +93,7 @@ def make_barrier_pricer(S0, K, sigma, rate, barrier_type, upper_barrier, lower_b
         use_one_sided_greeks_near_barrier=use_one_sided_greeks_near_barrier,
         num_space_nodes=num_space_nodes, num_time_steps=num_time_steps, grid_type=grid_type,
         rannacher_steps=2, restart_on_monitoring=False, mollify_final=False,
-        mollify_band_nodes=2, day_count=day_count, engine=engine)
+        mollify_band_nodes=2, day_count=day_count, engine=engine, grid_mode=grid_mode)
 
 
 def run_scenario(scenario_name: str, S0: float, K: float, sigma: float, rate: float,

@@ -83,8 +83,8 @@ def test_runner_reproduces_committed_results(cfg, res, tmp_path):
     df = scenarios.run_all_scenarios(_golden_csv(cfg), str(out),
                                      scenarios.runner_base_params("put", 500), engine=eng,
                                      verbose=False)
-    ref = pd.read_csv(_golden_csv(res))
-    got = pd.read_csv(out)
+    ref = pd.read_csv(_golden_csv(res), float_precision="round_trip")
+    got = pd.read_csv(out, float_precision="round_trip")
     assert list(got.columns) == list(ref.columns)
     assert list(got["scenario_name"]) == list(ref["scenario_name"])
     # The committed CSVs were written by the reference on another machine

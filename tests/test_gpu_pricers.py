@@ -1,0 +1,130 @@
+"""Pricer façades on the MI355X (HIP engine) against the reference.
+
+Tolerances (fp64; the kernel reassociates the Thomas solve, so agreement is
+to rounding, not bitwise):
+  price, delta:            |x - ref| <= 1e-10 + 1e-9 |ref|
+  gamma, theta, vega:      |x - ref| <= 1e-8 * max(1, |ref|)
+  value vectors:           max|V - V_ref| <= 1e-10 * max(1, max|V_ref|)
+"""
+import datetime as dt
+import math
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from backends import oracle_engine
+from conftest import GOLDEN, load_golden
+from finite_difference_amd import scenarios
+from finite_difference_amd.engine import Engine
+from finite_difference_amd.fd_barrier import FDDoubleBarrier
+
+pytestmark = pytest.mark.gpu
+
+TIGHT = {"price": (1e-10, 1e-9), "delta": (1e-10, 1e-9)}
+
+
+def close(name, x, ref):
+    atol, rtol = TIGHT.get(name, (1e-8, 1e-8))
+    return abs(x - ref) <= atol + rtol * abs(ref) if name in TIGHT else \
+        abs(x - ref) <= 1e-8 * max(1.0, abs(ref))
+
+
+def check_greeks(g, ref, label):
+    worst = {k: abs(g[k] - ref[k]) for k in ref}
+    print(f"[{label}] abs err {worst}")
+    for k in ref:
+        assert close(k, g[k], ref[k]), (label, k, g[k], ref[k])
+
+
+def test_american_golden_on_gpu():
+    import test_american_host as T
+    for case in T.CASES:
+        p = T.make(case, Engine())
+        assert close("price", p.price_log(), case["price_log"])
+        assert close("price", p.price_log2(), case["price_log2"])
+        check_greeks(p.greeks_log2(), case["greeks_log2"], "american " + case["name"])
+
+
+def test_american_config2_full_grid():
+    rec = load_golden("american_cases.json")["config2"]
+    from finite_difference_amd.american import AmericanFDMPricer
+    from finite_difference_amd import market
+    c = market.iso_curve(market.create_rate_df(math.exp(0.07053828272) - 1.0))
+    p = AmericanFDMPricer(spot=176.39, strike=170.0, valuation_date=dt.date(2025, 7, 28),
+                          maturity_date=dt.date(2025, 8, 28), sigma=0.296783211249,
+                          option_type="put", discount_curve=c, forward_curve=c,
+                          num_space_nodes=2048, num_time_steps=4096, rannacher_steps=2)
+    V = p._solve_grid()
+    assert len(V) == rec["V_len"]
+    for i, v in rec["V_sample"].items():
+        assert abs(V[int(i)] - v) <= 1e-10 * max(1.0, abs(v))
+    print(f"[config2] price {p.price_log()!r} ref {rec['price_log']!r}")
+    assert close("price", p.price_log(), rec["price_log"])
+
+
+def test_barrier_golden_on_gpu():
+    import test_barrier_host as T
+    for case in T.GOLD["cases"]:
+        p = T.make(case["inputs"], Engine())
+        assert close("price", p.price_log2(), case["price_log2"])
+        check_greeks(p.greeks_log2(), case["greeks_log2"], "barrier " + case["name"])
+
+
+@pytest.mark.parametrize("cfg,res", [("config_scenarios.csv", "scenario_results.csv"),
+                                     ("config_scenarios_space_1.csv", "scenario_results_1.csv")])
+def test_runner_committed_results_on_gpu(cfg, res, tmp_path):
+    out = tmp_path / "o.csv"
+    scenarios.run_all_scenarios(os.path.join(GOLDEN, "ref_csv", cfg), str(out),
+                                scenarios.runner_base_params("put", 500), verbose=False)
+    got = pd.read_csv(out, float_precision="round_trip")
+    ref = pd.read_csv(os.path.join(GOLDEN, "ref_csv", res), float_precision="round_trip")
+    for col in ("model_price", "model_delta", "model_gamma", "model_vega"):
+        err = float(np.max(np.abs(got[col].to_numpy() - ref[col].to_numpy())))
+        print(f"[{res}] {col} max abs err {err:.3e}")
+        assert err <= 1e-9
+
+
+def test_cn_log_golden_on_gpu():
+    import test_cn_log_host as T
+    for case in T.CASES:
+        p = T.make(case["inputs"], Engine())
+        assert close("price", p.price(), case["price"])
+        if "greeks" in case:
+            check_greeks(p.greeks(), case["greeks"], "cnlog " + case["inputs"]["name"])
+
+
+def test_config3_explicit_batch_sample_vs_oracle():
+    """BASELINE config 3 shape: 1024 x 2000 explicit grid, mixed barrier types."""
+    rng = np.random.default_rng(20250728)
+    base = scenarios.runner_base_params("put", 1024)
+    base["num_time_steps"] = 2000
+    base["grid_mode"] = "explicit"
+    rows = []
+    kinds = ["up-and-out", "down-and-out", "up-and-in", "down-and-in"]
+    for i in range(16):
+        bt = kinds[i % 4]
+        rows.append(dict(scenario_name=f"s{i}", S0=229.74, K=float(rng.uniform(150, 300)),
+                         sigma=float(rng.uniform(0.15, 0.45)), rate=0.073086, barrier_type=bt,
+                         upper_barrier=float(rng.uniform(1.02, 1.5) * 229.74) if "up" in bt else None,
+                         lower_barrier=float(rng.uniform(0.6, 0.98) * 229.74) if "down" in bt else None))
+    gpu = scenarios.run_rows(rows, dict(base, opt_type="call"))
+    ref = scenarios.run_rows(rows, dict(base, opt_type="call"), engine=oracle_engine())
+    for g, r in zip(gpu, ref):
+        for k in ("model_price", "model_delta"):
+            assert abs(g[k] - r[k]) <= 1e-10 + 1e-9 * abs(r[k]), (k, g[k], r[k])
+        for k in ("model_gamma", "model_vega"):
+            assert abs(g[k] - r[k]) <= 1e-8 * max(1.0, abs(r[k])), (k, g[k], r[k])
+
+
+def test_config5_double_barrier_full_grid_vs_oracle():
+    P = (20.786, 21.0, 19.0, 23.0, 0.10994120968)
+    b, r, T = 0.049493018, 0.0709454892, 49 / 365
+    d_gpu = FDDoubleBarrier(*P, "c", "out", n_space=4096, n_time=8192)
+    sv = d_gpu.solve_for(b, r, T)
+    Vg = Engine().run([sv])[0]
+    Vo = oracle_engine().run([sv])[0]
+    err = float(np.max(np.abs(Vg - Vo))) / max(1.0, float(np.max(np.abs(Vo))))
+    print(f"[config5] rel err {err:.3e} price {d_gpu.finish(Vg, b, r, T)}")
+    assert err <= 1e-10
