@@ -83,7 +83,8 @@ def test_runner_committed_results_on_gpu(cfg, res, tmp_path):
     for col in ("model_price", "model_delta", "model_gamma", "model_vega"):
         err = float(np.max(np.abs(got[col].to_numpy() - ref[col].to_numpy())))
         print(f"[{res}] {col} max abs err {err:.3e}")
-        assert err <= 1e-9
+        # price/delta: 1e-10 abs; gamma/vega (finite differences / 0.01): 1e-8
+        assert err <= (1e-10 if col in ("model_price", "model_delta") else 1e-8)
 
 
 def test_cn_log_golden_on_gpu():
