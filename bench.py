@@ -137,7 +137,7 @@ def main():
     g = build_workload(args.batch, args.n_space, args.n_time, seed=rank)
     t_build = time.perf_counter() - t_build
     k_cap = capi.sm_extent(g.n_nodes, g.n_time, g.n_ranna, g.params)
-    plan = capi.plan(g.n_nodes, True, k_cap)
+    plan = capi.plan(g.n_nodes, True, k_cap, n_time=g.n_time)
 
     P = torch.from_numpy(g.params).to(dev)
     I = torch.from_numpy(g.iparams).to(dev)
@@ -151,7 +151,7 @@ def main():
     def step():
         capi.it_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, P.data_ptr(), I.data_ptr(),
                           V0.data_ptr(), F.data_ptr(), out.data_ptr(), k_cap,
-                          ws.data_ptr() if plan["ws_bytes_per_scen"] else 0,
+                          ws.data_ptr(),
                           stream.cuda_stream)
 
     for _ in range(args.warmup):

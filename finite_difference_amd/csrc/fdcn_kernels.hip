@@ -70,6 +70,16 @@ __device__ __forceinline__ double read_lane(double x, int l) {
 
 __device__ __forceinline__ int uni_i(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// Hide an index from the optimiser for one loop iteration, so table loads
+// indexed by it are not hoisted out of the time loop (LICM would otherwise keep
+// every LDS table entry of the lane live in VGPRs for the whole march).  An
+// integer is hidden rather than the pointer so the LDS address space (and
+// ds_read) is kept.
+__device__ __forceinline__ int opaque(int i) {
+  asm volatile("" : "+v"(i));
+  return i;
+}
+
 __device__ __forceinline__ double shfl_up1(double x, int d) { return __shfl_up(x, (unsigned)d, 64); }
 __device__ __forceinline__ double shfl_dn1(double x, int d) { return __shfl_down(x, (unsigned)d, 64); }
 
@@ -152,9 +162,6 @@ __device__ __forceinline__ double pow_n(double x, int n) {
 // ---------------------------------------------------------------------------
 struct KArgs {
   int B, n_nodes, n_time, n_ranna, n_mon, lz;
-  int z_lds;    // SM table in LDS (1) or in the global workspace zg (0)
-  int phi_lds;  // IT payoff staged in LDS (1) or read from `payoff` (0)
-  double* zg;   // [B][2][NPT][lz] when !z_lds
   const double* params;
   const int32_t* iparams;
   const double* v_init;
@@ -162,24 +169,28 @@ struct KArgs {
   const int32_t* mon_step;
   const double* mon_rebate;
   double* v_out;
+  double* bnd;      // workspace: Dirichlet values [B][W][n_pad][2]
+  int n_pad;        // n_time rounded up to a multiple of 64
 };
 
 template <int IT, int W, int NPT>
 struct Geo {
   static constexpr int L = 64 * W;
-  static constexpr int SPB = (W == 1) ? 4 : 1;
+  static constexpr int SPB = 1;  // one scenario per workgroup (LDS sized per scenario)
+  // IT payoff staged in LDS unless it would not fit (8+ waves per scenario)
+  static constexpr bool kPhiLds = IT && (W <= 4);
   static constexpr int kThreads = 64 * W * SPB;
 };
 
 // doubles of LDS per scenario
 template <int IT, int W, int NPT>
-__host__ __device__ inline int lds_doubles_per_scen(int lz, int z_lds, int phi_lds) {
-  return (z_lds ? 2 * lz * NPT : 0) + ((IT && phi_lds) ? 64 * W * NPT : 0) +
+__host__ __device__ inline int lds_doubles_per_scen(int lz) {
+  return 2 * lz * (NPT + 1) + (Geo<IT, W, NPT>::kPhiLds ? 64 * W * NPT : 0) +
          (W > 1 ? Xch<W>::kSize : 0);
 }
 
 template <int IT, int W, int NPT>
-__global__ void __launch_bounds__((64 * W * ((W == 1) ? 4 : 1)))
+__global__ void __launch_bounds__(64 * W)
 fdcn_march(KArgs A) {
   constexpr int L = Geo<IT, W, NPT>::L;
   constexpr int SPB = Geo<IT, W, NPT>::SPB;
@@ -196,12 +207,11 @@ fdcn_march(KArgs A) {
   const int n_nodes = A.n_nodes;
   const int n_int = n_nodes - 2;
   const int lz = A.lz;
-  const int z_lds = A.z_lds, phi_lds = A.phi_lds;
-  double* my = lds + (size_t)scen_in_blk * lds_doubles_per_scen<IT, W, NPT>(lz, z_lds, phi_lds);
-  // SM table [2][NPT][lz]: LDS, or this scenario's slice of the global workspace
-  double* ztab = z_lds ? my : A.zg + (size_t)scen * 2 * NPT * lz;
-  double* phit = my + (z_lds ? 2 * lz * NPT : 0);  // [NPT][L] (IT, phi_lds)
-  double* xch = phit + ((IT && phi_lds) ? L * NPT : 0);  // exchange area (W > 1)
+  constexpr bool kPhiLds = Geo<IT, W, NPT>::kPhiLds;
+  double* my = lds + (size_t)scen_in_blk * lds_doubles_per_scen<IT, W, NPT>(lz);
+  double* ztab = my;                                  // SM table [2][lz][NPT+1]
+  double* phit = my + 2 * lz * (NPT + 1);             // payoff [NPT][L] (kPhiLds)
+  double* xch = phit + (kPhiLds ? L * NPT : 0);       // exchange area (W > 1)
   (void)xch;
 
   const double* P = A.params + (size_t)scen * FDCN_NPARAM;
@@ -212,6 +222,23 @@ fdcn_march(KArgs A) {
   const double cbc = uni(P[FDCN_P_BC]);
   const double tau0 = uni(P[FDCN_P_TAU0]);
 
+  // Dirichlet values of every step, evaluated once up front (while few
+  // registers are live) into this wave's workspace row: lane l owns steps
+  // m = l (mod 64) and is the only lane that reads them back, so no
+  // synchronisation is needed.  tau_m = tau0 + (m+1) dt (…pricer.py:519).
+  double2* bnd = reinterpret_cast<double2*>(A.bnd) + ((size_t)scen * W + wave) * A.n_pad;
+  {
+    const int lof = uni_i(I[FDCN_I_LO_FORM]), hif = uni_i(I[FDCN_I_HI_FORM]);
+    const double l0 = uni(P[FDCN_P_LO_C0]), l1 = uni(P[FDCN_P_LO_E0]),
+                 l2 = uni(P[FDCN_P_LO_C1]), l3 = uni(P[FDCN_P_LO_E1]);
+    const double h0 = uni(P[FDCN_P_HI_C0]), h1 = uni(P[FDCN_P_HI_E0]),
+                 h2 = uni(P[FDCN_P_HI_C1]), h3 = uni(P[FDCN_P_HI_E1]);
+    for (int m = lane; m < A.n_pad; m += 64) {
+      const double tau = tau0 + (double)(m + 1) * dt;
+      bnd[m] = make_double2(bnd_eval(lof, l0, l1, l2, l3, tau), bnd_eval(hif, h0, h1, h2, h3, tau));
+    }
+  }
+
   // lane geometry
   const int L_act = (n_int + NPT - 1) / NPT;
   const int L_short = L_act * NPT - n_int;
@@ -219,11 +246,21 @@ fdcn_march(KArgs A) {
   const bool shrt = t < L_short;
   const int s_t = t * NPT - (t < L_short ? t : L_short);  // first interior index
 
+  // ---- chunk decomposition for instruction-level parallelism -------------
+  // Each lane's NPT-node chunk is split into S sub-chains of M nodes.  The
+  // recurrences run the S sub-chains interleaved (independent FMA chains) and
+  // join them with a short Horner step in fm^M / bm^M, so a wave keeps S
+  // fp64 FMAs in flight instead of one dependent chain.
+  constexpr int S = (NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1);
+  constexpr int M = NPT / S;
+
   // ---- per-theta constants: scan window products + SM table -------------
   double FW[6], GW[6];
-  double Fpre = 0.0, Gsuf = 0.0, mlast = 0.0, glast = 0.0;
+  double Fpre = 0.0, Gsuf = 0.0;
+  double mlast = 0.0, glast = 0.0;  // phantom slot: pass-through multipliers
+  double mulLF = 0.0, mulLB = 0.0;  // products across the last sub-chain
+  double fmM = 0.0, bmM = 0.0;      // products across a full sub-chain
   Phase ph;
-  double smc = 0.0;
   double V[NPT];
   double LAM[NPT];
   (void)LAM;
@@ -232,14 +269,21 @@ fdcn_march(KArgs A) {
     if constexpr (W > 1) __syncthreads();  // previous readers of Ftot/Gtot are done
     mlast = shrt ? 1.0 : p.fm;
     glast = shrt ? 1.0 : p.bm;
+    const double fM1 = pow_n<NPT>(p.fm, M - 1), bM1 = pow_n<NPT>(p.bm, M - 1);
+    fmM = uni(fM1 * p.fm);
+    bmM = uni(bM1 * p.bm);
+    mulLF = shrt ? fM1 : fmM;
+    mulLB = shrt ? bM1 : bmM;
     const int len = shrt ? NPT - 1 : NPT;
     double f = active ? pow_n<NPT>(p.fm, len) : 0.0;
     double g = active ? pow_n<NPT>(p.bm, len) : 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      FW[j] = f;
-      GW[j] = g;
+      // zero where the shuffle source lane does not exist: the scan step
+      // b += FW*b_src then needs no lane mask
+      FW[j] = (lane >= d) ? f : 0.0;
+      GW[j] = (lane + d < 64) ? g : 0.0;
       const double fo = shfl_up1(f, d);
       const double go = shfl_dn1(g, d);
       f = (lane >= d) ? f * fo : f;
@@ -256,17 +300,27 @@ fdcn_march(KArgs A) {
 
   // forward + backward sweeps on V (rhs/r in, solution out), in place
   auto solve = [&](const Phase& p) __attribute__((always_inline)) {
-    // forward pass 1: chunk aggregate with zero carry
-    double w = 0.0;
+    const double fm = p.fm, bm = p.bm;
+    // forward pass 1: zero-carry end value of every sub-chain
+    double a[S];
 #pragma unroll
-    for (int k = 0; k < NPT - 1; ++k) w = fma(p.fm, w, V[k]);
-    w = fma(mlast, w, V[NPT - 1]);
-    double b = active ? w : 0.0;
+    for (int j = 0; j < S; ++j) {
+      double w = 0.0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int k = j * M + i;
+        w = fma(k == NPT - 1 ? mlast : fm, w, V[k]);
+      }
+      a[j] = w;
+    }
+    double e = a[0];
+#pragma unroll
+    for (int j = 1; j < S; ++j) e = fma(j == S - 1 ? mulLF : fmM, e, a[j]);
+    double b = active ? e : 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      const double o = shfl_up1(b, d);
-      if (lane >= d) b = fma(FW[j], o, b);
+      b = fma(FW[j], shfl_up1(b, d), b);
     }
     double cw = 0.0;
     if constexpr (W > 1) {
@@ -280,25 +334,42 @@ fdcn_march(KArgs A) {
     double cin = shfl_up1(b, 1);
     if (lane == 0) cin = cw;
     if (!active) cin = 0.0;
-    // forward pass 2
-    w = cin;
+    // forward pass 2: carries into every sub-chain, then S chains in parallel
+    double c[S];
+    c[0] = cin;
 #pragma unroll
-    for (int k = 0; k < NPT - 1; ++k) {
-      w = fma(p.fm, w, V[k]);
-      V[k] = w;
+    for (int j = 1; j < S; ++j) c[j] = fma(fmM, c[j - 1], a[j - 1]);
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      double w = c[j];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int k = j * M + i;
+        w = fma(k == NPT - 1 ? mlast : fm, w, V[k]);
+        V[k] = (k == NPT - 1 && shrt) ? 0.0 : w;
+      }
     }
-    w = fma(mlast, w, V[NPT - 1]);
-    V[NPT - 1] = shrt ? 0.0 : w;
-    // backward pass 1
-    double y = V[NPT - 1];  // glast * 0 + V
+    // backward pass 1: zero-carry start value of every sub-chain
 #pragma unroll
-    for (int k = NPT - 2; k >= 0; --k) y = fma(p.bm, y, V[k]);
-    double cb = active ? y : 0.0;
+    for (int j = 0; j < S; ++j) {
+      double y = 0.0;
+#pragma unroll
+      for (int i = M - 1; i >= 0; --i) {
+        const int k = j * M + i;
+        y = fma(k == NPT - 1 ? glast : bm, y, V[k]);
+      }
+      a[j] = y;
+    }
+    // zero-carry start value of the chunk: E_j = a[j] + prod(sub-chain j) E_{j+1};
+    // sub-chains j <= S-2 never hold the phantom slot, so the product is bm^M
+    e = a[S - 1];
+#pragma unroll
+    for (int j = S - 2; j >= 0; --j) e = fma(bmM, e, a[j]);
+    double cb = active ? e : 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      const double o = shfl_dn1(cb, d);
-      if (lane + d < 64) cb = fma(GW[j], o, cb);
+      cb = fma(GW[j], shfl_dn1(cb, d), cb);
     }
     double cwb = 0.0;
     if constexpr (W > 1) {
@@ -313,12 +384,18 @@ fdcn_march(KArgs A) {
     if (lane == 63) cinb = cwb;
     if (!active) cinb = 0.0;
     // backward pass 2
-    y = fma(glast, cinb, V[NPT - 1]);
-    V[NPT - 1] = y;
+    c[S - 1] = cinb;
 #pragma unroll
-    for (int k = NPT - 2; k >= 0; --k) {
-      y = fma(p.bm, y, V[k]);
-      V[k] = y;
+    for (int j = S - 2; j >= 0; --j) c[j] = fma(j + 1 == S - 1 ? mulLB : bmM, c[j + 1], a[j + 1]);
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      double y = c[j];
+#pragma unroll
+      for (int i = M - 1; i >= 0; --i) {
+        const int k = j * M + i;
+        y = fma(k == NPT - 1 ? glast : bm, y, V[k]);
+        V[k] = y;
+      }
     }
   };
 
@@ -343,7 +420,7 @@ fdcn_march(KArgs A) {
     solve(p);
     if (t < lz) {
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) ztab[(tab * NPT + k) * lz + t] = V[k];
+      for (int k = 0; k < NPT; ++k) ztab[(tab * lz + t) * (NPT + 1) + k] = V[k];
     }
     const double z0 = bcast_first(V[0]);
     return uni(p.kappa / (1.0 + p.kappa * z0));
@@ -351,19 +428,19 @@ fdcn_march(KArgs A) {
 
   const bool use_r = A.n_ranna > 0;
   const bool use_c = A.n_ranna < A.n_time;
-  const Phase pr = make_phase(1.0, dt, ca, cc, cbc);
-  const Phase pc = make_phase(0.5, dt, ca, cc, cbc);
   int kext = 1;
   double smc_r = 0.0, smc_c = 0.0;
   if (use_c) {
-    setup_scan(pc);
-    smc_c = build_sm(pc, 1);
-    kext = max(kext, sm_extent(pc.fm, n_int));
+    ph = make_phase(0.5, dt, ca, cc, cbc);
+    setup_scan(ph);
+    smc_c = build_sm(ph, 1);
+    kext = max(kext, sm_extent(ph.fm, n_int));
   }
   if (use_r) {
-    setup_scan(pr);
-    smc_r = build_sm(pr, 0);
-    kext = max(kext, sm_extent(pr.fm, n_int));
+    ph = make_phase(1.0, dt, ca, cc, cbc);
+    setup_scan(ph);
+    smc_r = build_sm(ph, 0);
+    kext = max(kext, sm_extent(ph.fm, n_int));
   }
   // nodes covered by the first lz lanes; a larger extent means the table is
   // too small for this scenario: poison the output (loud, never silently off)
@@ -384,16 +461,10 @@ fdcn_march(KArgs A) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int node = s_t + 1 + k;
-      if (phi_lds) phit[k * L + t] = (active && node <= n_int) ? pin[node] : 0.0;
+      if constexpr (kPhiLds) phit[k * L + t] = (active && node <= n_int) ? pin[node] : 0.0;
       LAM[k] = 0.0;
     }
   }
-  const int lo_form = uni_i(I[FDCN_I_LO_FORM]);
-  const int hi_form = uni_i(I[FDCN_I_HI_FORM]);
-  const double lc0 = P[FDCN_P_LO_C0], le0 = P[FDCN_P_LO_E0], lc1 = P[FDCN_P_LO_C1],
-               le1 = P[FDCN_P_LO_E1];
-  const double hc0 = P[FDCN_P_HI_C0], he0 = P[FDCN_P_HI_E0], hc1 = P[FDCN_P_HI_C1],
-               he1 = P[FDCN_P_HI_E1];
   const int ko_lo = uni_i(I[FDCN_I_KO_LO]);
   const int ko_hi = uni_i(I[FDCN_I_KO_HI]);
   int mpos = uni_i(I[FDCN_I_MON_START]);
@@ -404,33 +475,36 @@ fdcn_march(KArgs A) {
     if (lane == 0) xch[Xch<W>::kFirst + wave] = V[0];
     if (lane == 63) xch[Xch<W>::kLast + wave] = shrt ? V[NPT - 2] : V[NPT - 1];
   }
-  // phase for step 0
+  // phase for step 0 (ph currently holds the theta the last table was built for)
+  double smc;
+  int tab;
   if (use_r) {
-    ph = pr;
     smc = smc_r;
+    tab = 0;
   } else {
-    setup_scan(pc);  // tables built; recompute c-phase window products
-    ph = pc;
+    ph = make_phase(0.5, dt, ca, cc, cbc);
+    setup_scan(ph);
     smc = smc_c;
+    tab = 1;
   }
-  int tab = use_r ? 0 : 1;
   const double inv_dt = uni(1.0 / dt);
+  const double neg_dt = uni(-dt);
 
-  double lo_reg = 0.0, hi_reg = 0.0;
+  double2 bnd_cur = make_double2(0.0, 0.0);
+  double2 bnd_nxt = bnd[lane];  // steps 0..63
   for (int m = 0; m < A.n_time; ++m) {
     if (m == A.n_ranna && use_r) {  // Rannacher -> Crank-Nicolson
-      setup_scan(pc);
-      ph = pc;
+      ph = make_phase(0.5, dt, ca, cc, cbc);
+      setup_scan(ph);
       smc = smc_c;
       tab = 1;
     }
-    if ((m & 63) == 0) {  // Dirichlet values for the next 64 steps, one per lane
-      const double tau = tau0 + (double)(m + lane + 1) * dt;
-      lo_reg = bnd_eval(lo_form, lc0, le0, lc1, le1, tau);
-      hi_reg = bnd_eval(hi_form, hc0, he0, hc1, he1, tau);
+    if ((m & 63) == 0) {  // Dirichlet values of the next 64 steps, one per lane
+      bnd_cur = bnd_nxt;
+      if (m + 64 < A.n_pad) bnd_nxt = bnd[m + 64 + lane];  // prefetch the block after
     }
-    const double lo_new = read_lane(lo_reg, m & 63);
-    const double hi_new = read_lane(hi_reg, m & 63);
+    const double lo_new = read_lane(bnd_cur.x, m & 63);
+    const double hi_new = read_lane(bnd_cur.y, m & 63);
 
     // ---- 1. rhs/r ----------------------------------------------------------
     if constexpr (W > 1) __syncthreads();  // halos of the previous step
@@ -446,15 +520,34 @@ fdcn_march(KArgs A) {
     if (!active) { left = 0.0; right = 0.0; }
     if (shrt) V[NPT - 1] = right;
     {
+      // r_k = fma(bl, V_{k-1}, fma(bc, V_k, bu V_{k+1})) (+ dt/r lambda_k), in
+      // place: the old V_k is saved for node k+1 before it is overwritten.
+      // Written as asm so the compiler cannot evaluate all rhs values ahead
+      // of the stores (which doubles the live state and the VGPR count).
       double prev = left;
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
-        const double cur = V[k];
         const double nxt = (k < NPT - 1) ? V[k + 1] : right;
-        double r = fma(ph.bl, prev, fma(ph.bc, cur, ph.bu * nxt));
-        if constexpr (IT) r = fma(ph.dtr, LAM[k], r);
-        V[k] = r;
-        prev = cur;
+        double saved;
+        if constexpr (IT) {
+          asm volatile(
+              "v_mov_b64 %1, %0\n\t"
+              "v_mul_f64 %0, %3, %2\n\t"
+              "v_fma_f64 %0, %4, %1, %0\n\t"
+              "v_fma_f64 %0, %5, %6, %0\n\t"
+              "v_fma_f64 %0, %7, %8, %0"
+              : "+v"(V[k]), "=&v"(saved)
+              : "v"(nxt), "s"(ph.bu), "s"(ph.bc), "s"(ph.bl), "v"(prev), "s"(ph.dtr), "v"(LAM[k]));
+        } else {
+          asm volatile(
+              "v_mov_b64 %1, %0\n\t"
+              "v_mul_f64 %0, %3, %2\n\t"
+              "v_fma_f64 %0, %4, %1, %0\n\t"
+              "v_fma_f64 %0, %5, %6, %0"
+              : "+v"(V[k]), "=&v"(saved)
+              : "v"(nxt), "s"(ph.bu), "s"(ph.bc), "s"(ph.bl), "v"(prev));
+        }
+        prev = saved;
       }
     }
     if (t == 0) V[0] = fma(ph.fm, lo_new, V[0]);
@@ -463,55 +556,55 @@ fdcn_march(KArgs A) {
 
     // ---- 2. tridiagonal solve ---------------------------------------------
     solve(ph);
-    {
-      const bool need = (W == 1) || (lz > 64) || (wave == 0);
-      if (need) {
-        double y0;
-        if constexpr (W == 1) {
-          y0 = read_lane(V[0], 0);
-        } else {
-          if (lz > 64) {
-            y0 = bcast_first(V[0]);
-          } else {
-            y0 = read_lane(V[0], 0);
-          }
-        }
-        const double g = smc * y0;
-        if (t < lz) {
-          const double* zt = ztab + tab * NPT * lz;
-#pragma unroll
-          for (int k = 0; k < NPT; ++k) V[k] = fma(-g, zt[k * lz + t], V[k]);
-        }
+    // Sherman-Morrison: x = y - (k y0 / (1 + k z0)) z over the first lz lanes.
+    // Branch-free (a zero multiplier outside): a divergent branch here makes
+    // the compiler keep two copies of V live.
+    if ((W == 1) || (lz > 64) || (wave == 0)) {
+      double y0;
+      if constexpr (W == 1) {
+        y0 = read_lane(V[0], 0);
+      } else {
+        y0 = (lz > 64) ? bcast_first(V[0]) : read_lane(V[0], 0);
       }
+      const double g = (t < lz) ? -(smc * y0) : 0.0;
+      // lane-major rows (stride NPT+1: bank-spread, immediate offsets);
+      // lanes >= lz read row lz-1 with g = 0
+      const int off = opaque((tab * lz + (t < lz ? t : lz - 1)) * (NPT + 1));
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) V[k] = fma(g, ztab[off + k], V[k]);
     }
 
     // ---- 3. early exercise / boundaries / knock-out ------------------------
     if constexpr (IT) {
+      // fd_american_equity.py:704-717; max() differs from the reference's
+      // compare-select only in the sign of an exact zero
+      const int off = opaque(kPhiLds ? t : s_t + 1);
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
-        const double tv = V[k];
         const int node = s_t + 1 + k;
-        const double pk = phi_lds ? phit[k * L + t]
-                                  : ((active && node <= n_int) ? pin[node] : 0.0);
-        const double lam = LAM[k];
-        const double cand = fma(-dt, lam, tv);
-        V[k] = pk > cand ? pk : cand;
-        const double ln = fma(pk - tv, inv_dt, lam);
-        LAM[k] = ln < 0.0 ? 0.0 : ln;
+        const double pk = kPhiLds ? phit[off + k * L]
+                                  : ((active && node <= n_int) ? pin[off + k] : 0.0);
+        // V = max(phi, V - dt lam);  lam = max(lam + (phi - V_old)/dt, 0), in place
+        double d;
+        asm volatile(
+            "v_add_f64 %2, %3, -%0\n\t"
+            "v_fma_f64 %0, %4, %1, %0\n\t"
+            "v_max_f64 %0, %3, %0\n\t"
+            "v_fma_f64 %1, %2, %5, %1\n\t"
+            "v_max_f64 %1, %1, 0"
+            : "+v"(V[k]), "+v"(LAM[k]), "=&v"(d)
+            : "v"(pk), "s"(neg_dt), "s"(inv_dt));
       }
       if (shrt) LAM[NPT - 1] = 0.0;
     }
     V0 = lo_new;
     VN = hi_new;
-    if (m + 1 == next_mon) {
+    if (m + 1 == next_mon) {  // knock-out projection (uniform branch, per-node select)
       const double reb = uni(A.mon_rebate[mpos]);
-      if (active) {
+      const int klo = active ? ko_lo - s_t - 1 : -1;        // slots k <= klo are out
+      const int khi = active ? ko_hi - s_t - 1 : NPT + 1;   // slots k >= khi are out
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-          const int node = s_t + 1 + k;
-          if (node <= ko_lo || node >= ko_hi) V[k] = reb;
-        }
-      }
+      for (int k = 0; k < NPT; ++k) V[k] = (k <= klo || k >= khi) ? reb : V[k];
       if (0 <= ko_lo) V0 = reb;
       if (n_nodes - 1 >= ko_hi) VN = reb;
       ++mpos;
@@ -568,12 +661,13 @@ struct Variant {
   int it, w, npt;
   KernelFn fn;
   int threads, spb;
+  int (*lds_per_scen)(int lz);  // the kernel's own LDS layout, in doubles
 };
 
 template <int IT, int W, int NPT>
 Variant mk() {
   return Variant{IT, W, NPT, &fdcn_march<IT, W, NPT>, Geo<IT, W, NPT>::kThreads,
-                 Geo<IT, W, NPT>::SPB};
+                 Geo<IT, W, NPT>::SPB, &lds_doubles_per_scen<IT, W, NPT>};
 }
 
 #define FDCN_VARIANTS(IT)                                                                   \
@@ -584,31 +678,23 @@ Variant mk() {
 const Variant kVariants[] = {FDCN_VARIANTS(0), FDCN_VARIANTS(1)};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-int lds_doubles(const Variant& v, int lz, int z_lds, int phi_lds) {
-  int per = (z_lds ? 2 * lz * v.npt : 0) + ((v.it && phi_lds) ? 64 * v.w * v.npt : 0) +
-            (v.w > 1 ? 6 * v.w + 2 : 0);
-  return per * v.spb;
+// Lanes whose chunks must hold the Sherman-Morrison table to cover k_cap nodes.
+int lz_for(const Variant& v, int n_int, int k_cap) {
+  const int L_act = (n_int + v.npt - 1) / v.npt;
+  const int L_short = L_act * v.npt - n_int;
+  int lz = (k_cap + v.npt - 1) / v.npt;
+  if (lz < 1) lz = 1;
+  while (lz < L_act && lz * v.npt - (lz < L_short ? lz : L_short) < k_cap) ++lz;
+  if (lz > L_act) lz = L_act;
+  return lz;
 }
 
+int lds_doubles(const Variant& v, int lz);
 constexpr size_t kLdsLimit = 160 * 1024;
 
-// Table placement: everything in LDS when it fits; otherwise the SM table
-// (read by the first few lanes only) moves to the global workspace first, then
-// the payoff (read from the input array, L2-resident).
-void placement(const Variant& v, int lz, int* z_lds, int* phi_lds, size_t* lds_bytes) {
-  *z_lds = 1;
-  *phi_lds = 1;
-  *lds_bytes = sizeof(double) * (size_t)lds_doubles(v, lz, 1, 1);
-  if (*lds_bytes <= kLdsLimit) return;
-  *z_lds = 0;
-  *lds_bytes = sizeof(double) * (size_t)lds_doubles(v, lz, 0, 1);
-  if (*lds_bytes <= kLdsLimit) return;
-  *phi_lds = 0;
-  *lds_bytes = sizeof(double) * (size_t)lds_doubles(v, lz, 0, 0);
-}
-
-// Choose the variant: fewest waves per scenario, then the least padding.
-const Variant* choose(int n_nodes, int it) {
+// Choose the variant: fewest waves per scenario, then the least padding,
+// among those whose LDS (correction table + payoff) fits one CU.
+const Variant* choose(int n_nodes, int it, int k_cap) {
   const int n_int = n_nodes - 2;
   if (n_int < 3) return nullptr;
   const Variant* best = nullptr;
@@ -621,6 +707,8 @@ const Variant* choose(int n_nodes, int it) {
     const int L_act = (n_int + v.npt - 1) / v.npt;
     const int L_short = L_act * v.npt - n_int;
     if (L_act > 64 * v.w || L_short >= L_act || v.npt > n_int) continue;
+    const int kc = k_cap > 0 ? k_cap : (n_int < 256 ? n_int : 256);
+    if (sizeof(double) * (size_t)lds_doubles(v, lz_for(v, n_int, kc)) > kLdsLimit) continue;
     const long slots = (long)64 * v.w * v.npt;
     if (!best || v.w < best_w || slots < best_slots) {
       best = &v;
@@ -631,15 +719,17 @@ const Variant* choose(int n_nodes, int it) {
   return best;
 }
 
-// Lanes whose chunks must hold the Sherman-Morrison table to cover k_cap nodes.
-int lz_for(const Variant& v, int n_int, int k_cap) {
-  const int L_act = (n_int + v.npt - 1) / v.npt;
-  const int L_short = L_act * v.npt - n_int;
-  int lz = (k_cap + v.npt - 1) / v.npt;
-  if (lz < 1) lz = 1;
-  while (lz < L_act && lz * v.npt - (lz < L_short ? lz : L_short) < k_cap) ++lz;
-  if (lz > L_act) lz = L_act;
-  return lz;
+int lds_doubles(const Variant& v, int lz) { return v.lds_per_scen(lz) * v.spb; }
+
+
+
+
+
+int pad64(int n) { return ((n > 0 ? n : 1) + 63) / 64 * 64; }
+
+// workspace bytes per scenario: one (lo, hi) Dirichlet pair per step and wave
+size_t ws_bytes_per_scen(const Variant& v, int n_time) {
+  return sizeof(double) * 2 * (size_t)pad64(n_time) * (size_t)v.w;
 }
 
 double host_fm(double theta, const double* P) {
@@ -667,23 +757,15 @@ int launch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   int rc = validate_common(B, n_nodes, n_time, n_ranna);
   if (rc) return rc;
   if (B == 0) return FDCN_OK;
-  const Variant* v = choose(n_nodes, it);
+  const Variant* v = choose(n_nodes, it, k_cap);
   if (!v) return fail(FDCN_EINVAL, "unsupported n_nodes=%d", n_nodes);
   const int n_int = n_nodes - 2;
   if (k_cap <= 0) k_cap = n_int < 256 ? n_int : 256;
   const int lz = lz_for(*v, n_int, k_cap);
-  int z_lds, phi_lds;
-  size_t lds;
-  placement(*v, lz, &z_lds, &phi_lds, &lds);
+  const size_t lds = sizeof(double) * (size_t)lds_doubles(*v, lz);
   if (lds > kLdsLimit)
     return fail(FDCN_EINVAL, "LDS request %zu B too large (k_cap=%d)", lds, k_cap);
-  if (!z_lds && !workspace)
-    return fail(FDCN_EINVAL, "this size needs a workspace of %lld B per scenario (fdcn_plan)",
-                (long long)(sizeof(double) * 2 * (size_t)v->npt * lz));
   KArgs a;
-  a.z_lds = z_lds;
-  a.phi_lds = phi_lds;
-  a.zg = workspace;
   a.B = B;
   a.n_nodes = n_nodes;
   a.n_time = n_time;
@@ -697,12 +779,21 @@ int launch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   a.mon_step = mon_step;
   a.mon_rebate = mon_rebate;
   a.v_out = v_out;
+  a.n_pad = pad64(n_time);
+  const size_t ws_bytes = ws_bytes_per_scen(*v, n_time) * (size_t)B;
+  bool own_ws = false;
+  if (!workspace) {  // stream-ordered scratch, released after the launch
+    HIP_TRY(hipMallocAsync((void**)&workspace, ws_bytes, stream));
+    own_ws = true;
+  }
+  a.bnd = workspace;
   if (lds > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute((const void*)v->fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
   const int grid = (B + v->spb - 1) / v->spb;
   hipLaunchKernelGGL(v->fn, dim3(grid), dim3(v->threads), lds, stream, a);
   HIP_TRY(hipGetLastError());
+  if (own_ws) HIP_TRY(hipFreeAsync(workspace, stream));
   return FDCN_OK;
 }
 
@@ -777,7 +868,7 @@ int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ran
   {
     int32_t w_, npt_, spb_, lds_;
     int64_t ws_ = 0;
-    rc = fdcn_plan(n_nodes, it, k_cap, &w_, &npt_, &spb_, &lds_, &ws_);
+    rc = fdcn_plan(n_nodes, n_time, it, k_cap, &w_, &npt_, &spb_, &lds_, &ws_);
     if (rc == FDCN_OK && ws_ > 0 && hipMalloc((void**)&dW, (size_t)ws_ * B) != hipSuccess) {
       cleanup();
       return fail(FDCN_ENOMEM, "hipMalloc(workspace) failed");
@@ -818,23 +909,22 @@ int fdcn_sm_extent(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   return k;
 }
 
-int fdcn_plan(int32_t n_nodes, int32_t it_mode, int32_t k_cap, int32_t* waves, int32_t* npt,
-              int32_t* scen_per_block, int32_t* lds_bytes, int64_t* ws_bytes_per_scen) {
-  const Variant* v = choose(n_nodes, it_mode ? 1 : 0);
+int fdcn_plan(int32_t n_nodes, int32_t n_time, int32_t it_mode, int32_t k_cap, int32_t* waves,
+              int32_t* npt, int32_t* scen_per_block, int32_t* lds_bytes,
+              int64_t* ws_bytes_per_scen) {
+  if (n_time < 0) return fail(FDCN_EINVAL, "n_time must be >= 0 (got %d)", n_time);
+  const Variant* v = choose(n_nodes, it_mode ? 1 : 0, k_cap);
   if (!v) return fail(FDCN_EINVAL, "unsupported n_nodes=%d", n_nodes);
   const int n_int = n_nodes - 2;
   if (k_cap <= 0) k_cap = n_int < 256 ? n_int : 256;
   const int lz = lz_for(*v, n_int, k_cap);
-  int z_lds, phi_lds;
-  size_t lds;
-  placement(*v, lz, &z_lds, &phi_lds, &lds);
+  const size_t lds = sizeof(double) * (size_t)lds_doubles(*v, lz);
   if (lds > kLdsLimit) return fail(FDCN_EINVAL, "LDS request %zu B too large", lds);
   if (waves) *waves = v->w;
   if (npt) *npt = v->npt;
   if (scen_per_block) *scen_per_block = v->spb;
   if (lds_bytes) *lds_bytes = (int32_t)lds;
-  if (ws_bytes_per_scen)
-    *ws_bytes_per_scen = z_lds ? 0 : (int64_t)(sizeof(double) * 2 * (size_t)v->npt * lz);
+  if (ws_bytes_per_scen) *ws_bytes_per_scen = (int64_t)::ws_bytes_per_scen(*v, n_time);
   return FDCN_OK;
 }
 

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define FDCN_ABI_VERSION 1
+#define FDCN_ABI_VERSION 2
 
 /* ---- per-scenario fp64 parameters: params[b*FDCN_NPARAM + k] ---------- */
 enum fdcn_param {
@@ -111,15 +111,16 @@ int fdcn_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
 
 /* ---- device-pointer entry points (all pointers are device memory) ----- */
 /* `stream` is a hipStream_t (NULL = default stream); the call is
- * asynchronous on that stream and performs no allocation or host sync, so
- * it may be captured into a hipGraph.  Inputs and output may alias
- * (v_out == v_init) only if `v_init` is not needed afterwards.
+ * asynchronous on that stream and performs no host sync.  Inputs and output
+ * may alias (v_out == v_init) only if `v_init` is not needed afterwards.
  * `k_cap` bounds the boundary-layer correction table (see fdcn_sm_extent);
  * pass the value fdcn_sm_extent returns for the same params.  A scenario whose
  * extent exceeds k_cap gets NaN outputs (loud, never silently wrong).
  * `workspace` is device scratch of B * ws_bytes_per_scen bytes as reported by
- * fdcn_plan for the same (n_nodes, mode, k_cap); NULL when that is 0 (the
- * usual case: the correction table then lives in LDS). */
+ * fdcn_plan for the same (n_nodes, n_time, mode, k_cap): the Dirichlet values
+ * of every step are evaluated there once per launch.  With NULL the library
+ * allocates it stream-ordered (hipMallocAsync/hipFreeAsync on `stream`);
+ * pass a buffer to keep the call allocation-free (e.g. for hipGraph capture). */
 int fdcn_cn_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                       const double* params, const int32_t* iparams,
                       const double* v_init,
@@ -134,11 +135,11 @@ int fdcn_it_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_rann
 /* ---- launch planning / introspection ---------------------------------- */
 /* Writes the kernel geometry chosen for a launch: waves per scenario,
  * nodes per lane, scenarios per workgroup, LDS bytes per workgroup, and the
- * device workspace the _dev entry points need per scenario (0 = none).
+ * device workspace the _dev entry points need per scenario.
  * Any output pointer may be NULL.  Returns FDCN_EINVAL if the size is
  * unsupported. */
-int fdcn_plan(int32_t n_nodes, int32_t it_mode, int32_t k_cap, int32_t* waves,
-              int32_t* npt, int32_t* scen_per_block, int32_t* lds_bytes,
+int fdcn_plan(int32_t n_nodes, int32_t n_time, int32_t it_mode, int32_t k_cap,
+              int32_t* waves, int32_t* npt, int32_t* scen_per_block, int32_t* lds_bytes,
               int64_t* ws_bytes_per_scen);
 
 /* Extent (nodes) of the Sherman-Morrison boundary-layer correction needed by

@@ -11,5 +11,5 @@ rc=$?; echo "tests rc=$rc" >> gpurun_out/${TAG}_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py "$@" > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o ${TAG} -- \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o ${TAG} -- \
     python bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/${TAG}_prof.log 2>&1
