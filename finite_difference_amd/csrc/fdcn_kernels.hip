@@ -93,7 +93,6 @@ __device__ __forceinline__ double bnd_eval(int form, double c0, double e0, doubl
 struct Phase {
   double bl, bc, bu;  // B_L/r, B_C/r, B_U/r
   double fm, bm;      // -A_L/r, -A_U/r
-  double dtr;         // dt/r (Ikonen-Toivanen rhs term)
   double inv_r;
   double kappa;       // A_L A_U / r
 };
@@ -116,7 +115,6 @@ __device__ __forceinline__ Phase make_phase(double theta, double dt, double a, d
   p.bu = BU * p.inv_r;
   p.fm = -AL * p.inv_r;
   p.bm = -AU * p.inv_r;
-  p.dtr = dt * p.inv_r;
   p.kappa = AL * AU * p.inv_r;
   // wave-uniform: keep in SGPRs
   p.inv_r = uni(p.inv_r);
@@ -125,7 +123,6 @@ __device__ __forceinline__ Phase make_phase(double theta, double dt, double a, d
   p.bu = uni(p.bu);
   p.fm = uni(p.fm);
   p.bm = uni(p.bm);
-  p.dtr = uni(p.dtr);
   p.kappa = uni(p.kappa);
   return p;
 }
@@ -260,10 +257,11 @@ fdcn_march(KArgs A) {
   double mlast = 0.0, glast = 0.0;  // phantom slot: pass-through multipliers
   double mulLF = 0.0, mulLB = 0.0;  // products across the last sub-chain
   double fmM = 0.0, bmM = 0.0;      // products across a full sub-chain
+  int nst_f = 6, nst_b = 6;         // scan stages that carry weight above 1e-18
   Phase ph;
   double V[NPT];
-  double LAM[NPT];
-  (void)LAM;
+  double MU[NPT];  // Ikonen-Toivanen multiplier, stored scaled: mu = dt * lambda
+  (void)MU;
 
   auto setup_scan = [&](const Phase& p) __attribute__((always_inline)) {
     if constexpr (W > 1) __syncthreads();  // previous readers of Ftot/Gtot are done
@@ -291,6 +289,19 @@ fdcn_march(KArgs A) {
     }
     Fpre = f;
     Gsuf = g;
+    // After j Hillis-Steele stages lane t holds the contributions of lanes
+    // t-2^j+1..t; the rest is scaled by at most q^(2^j), q = |fm|^(NPT-1)
+    // (a short lane's product, the largest).  Stop once that is <= 1e-18:
+    // the dropped part is then ~1e-18 of the carried values, below fp64
+    // rounding (the same criterion as the Sherman-Morrison extent).
+    {
+      double qf = fabs(pow_n<NPT>(p.fm, NPT - 1)), qb = fabs(pow_n<NPT>(p.bm, NPT - 1));
+      int nf = 0, nb = 0;
+      while (nf < 6 && qf > 1e-18) { qf *= qf; ++nf; }
+      while (nb < 6 && qb > 1e-18) { qb *= qb; ++nb; }
+      nst_f = uni_i(nf);
+      nst_b = uni_i(nb);
+    }
     if constexpr (W > 1) {
       if (lane == 63) xch[Xch<W>::kFtot + wave] = Fpre;
       if (lane == 0) xch[Xch<W>::kGtot + wave] = Gsuf;
@@ -320,7 +331,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      b = fma(FW[j], shfl_up1(b, d), b);
+      if (j < nst_f) b = fma(FW[j], shfl_up1(b, d), b);
     }
     double cw = 0.0;
     if constexpr (W > 1) {
@@ -369,7 +380,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      cb = fma(GW[j], shfl_dn1(cb, d), cb);
+      if (j < nst_b) cb = fma(GW[j], shfl_dn1(cb, d), cb);
     }
     double cwb = 0.0;
     if constexpr (W > 1) {
@@ -462,7 +473,7 @@ fdcn_march(KArgs A) {
     for (int k = 0; k < NPT; ++k) {
       const int node = s_t + 1 + k;
       if constexpr (kPhiLds) phit[k * L + t] = (active && node <= n_int) ? pin[node] : 0.0;
-      LAM[k] = 0.0;
+      MU[k] = 0.0;
     }
   }
   const int ko_lo = uni_i(I[FDCN_I_KO_LO]);
@@ -487,8 +498,6 @@ fdcn_march(KArgs A) {
     smc = smc_c;
     tab = 1;
   }
-  const double inv_dt = uni(1.0 / dt);
-  const double neg_dt = uni(-dt);
 
   double2 bnd_cur = make_double2(0.0, 0.0);
   double2 bnd_nxt = bnd[lane];  // steps 0..63
@@ -537,7 +546,7 @@ fdcn_march(KArgs A) {
               "v_fma_f64 %0, %5, %6, %0\n\t"
               "v_fma_f64 %0, %7, %8, %0"
               : "+v"(V[k]), "=&v"(saved)
-              : "v"(nxt), "s"(ph.bu), "s"(ph.bc), "s"(ph.bl), "v"(prev), "s"(ph.dtr), "v"(LAM[k]));
+              : "v"(nxt), "s"(ph.bu), "s"(ph.bc), "s"(ph.bl), "v"(prev), "s"(ph.inv_r), "v"(MU[k]));
         } else {
           asm volatile(
               "v_mov_b64 %1, %0\n\t"
@@ -584,25 +593,28 @@ fdcn_march(KArgs A) {
         const int node = s_t + 1 + k;
         const double pk = kPhiLds ? phit[off + k * L]
                                   : ((active && node <= n_int) ? pin[off + k] : 0.0);
-        // V = max(phi, V - dt lam);  lam = max(lam + (phi - V_old)/dt, 0), in place
-        double d;
+        // fd_american_equity.py:704-717 with mu = dt*lambda:
+        //   v~ = V - mu;  mu' = max(phi - v~, 0);  V' = max(phi, v~)
+        // (= dt * max(lambda + (phi - V)/dt, 0) and max(phi, V - dt lambda)
+        // in exact arithmetic; 4 instructions, in place)
         asm volatile(
-            "v_add_f64 %2, %3, -%0\n\t"
-            "v_fma_f64 %0, %4, %1, %0\n\t"
-            "v_max_f64 %0, %3, %0\n\t"
-            "v_fma_f64 %1, %2, %5, %1\n\t"
-            "v_max_f64 %1, %1, 0"
-            : "+v"(V[k]), "+v"(LAM[k]), "=&v"(d)
-            : "v"(pk), "s"(neg_dt), "s"(inv_dt));
+            "v_add_f64 %0, %0, -%1\n\t"
+            "v_add_f64 %1, %2, -%0\n\t"
+            "v_max_f64 %1, %1, 0\n\t"
+            "v_max_f64 %0, %2, %0"
+            : "+v"(V[k]), "+v"(MU[k])
+            : "v"(pk));
       }
-      if (shrt) LAM[NPT - 1] = 0.0;
+      if (shrt) MU[NPT - 1] = 0.0;
     }
     V0 = lo_new;
     VN = hi_new;
-    if (m + 1 == next_mon) {  // knock-out projection (uniform branch, per-node select)
+    if (!IT && m + 1 == next_mon) {  // knock-out projection (uniform branch, per-node select)
       const double reb = uni(A.mon_rebate[mpos]);
-      const int klo = active ? ko_lo - s_t - 1 : -1;        // slots k <= klo are out
-      const int khi = active ? ko_hi - s_t - 1 : NPT + 1;   // slots k >= khi are out
+      // opaque: keep the per-slot masks inside this rare branch (hoisted out
+      // of the loop they would pin 2*NPT SGPRs for the whole march)
+      const int klo = opaque(active ? ko_lo - s_t - 1 : -1);       // slots k <= klo are out
+      const int khi = opaque(active ? ko_hi - s_t - 1 : NPT + 1);  // slots k >= khi are out
 #pragma unroll
       for (int k = 0; k < NPT; ++k) V[k] = (k <= klo || k >= khi) ? reb : V[k];
       if (0 <= ko_lo) V0 = reb;
