@@ -260,6 +260,7 @@ fdcn_march(KArgs A) {
   int nst_f = 6, nst_b = 6;         // scan stages that carry weight above 1e-18
   Phase ph;
   double V[NPT];
+  double X = 0.0;  // node 0 of the shifted RHS layout (see solve)
   double MU[NPT];  // Ikonen-Toivanen multiplier, stored scaled: mu = dt * lambda
   (void)MU;
 
@@ -309,7 +310,13 @@ fdcn_march(KArgs A) {
     }
   };
 
-  // forward + backward sweeps on V (rhs/r in, solution out), in place
+  // Forward + backward sweeps.  Input: rhs/r in the SHIFTED layout left by
+  // the in-place RHS (node 0 in X, node k >= 1 in V[k-1]); output: the
+  // solution in the natural layout (node k in V[k]).  The forward pass works
+  // in place on the shifted slots; the last backward pass writes node k into
+  // V[k] while reading node k's forward value from V[k-1], which undoes the
+  // shift at no cost.
+  auto R = [&](int k) -> double& { return k == 0 ? X : V[k - 1]; };
   auto solve = [&](const Phase& p) __attribute__((always_inline)) {
     const double fm = p.fm, bm = p.bm;
     // forward pass 1: zero-carry end value of every sub-chain
@@ -320,7 +327,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const int k = j * M + i;
-        w = fma(k == NPT - 1 ? mlast : fm, w, V[k]);
+        w = fma(k == NPT - 1 ? mlast : fm, w, R(k));
       }
       a[j] = w;
     }
@@ -356,8 +363,8 @@ fdcn_march(KArgs A) {
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const int k = j * M + i;
-        w = fma(k == NPT - 1 ? mlast : fm, w, V[k]);
-        V[k] = (k == NPT - 1 && shrt) ? 0.0 : w;
+        w = fma(k == NPT - 1 ? mlast : fm, w, R(k));
+        R(k) = (k == NPT - 1 && shrt) ? 0.0 : w;
       }
     }
     // backward pass 1: zero-carry start value of every sub-chain
@@ -367,7 +374,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
       for (int i = M - 1; i >= 0; --i) {
         const int k = j * M + i;
-        y = fma(k == NPT - 1 ? glast : bm, y, V[k]);
+        y = fma(k == NPT - 1 ? glast : bm, y, R(k));
       }
       a[j] = y;
     }
@@ -394,7 +401,11 @@ fdcn_march(KArgs A) {
     double cinb = shfl_dn1(cb, 1);
     if (lane == 63) cinb = cwb;
     if (!active) cinb = 0.0;
-    // backward pass 2
+    // backward pass 2 (unshifting).  Sub-chain j-1 writes V[jM-1], which
+    // holds sub-chain j's last input (node jM): read those first.
+    double wbot[S];
+#pragma unroll
+    for (int j = 1; j < S; ++j) wbot[j] = R(j * M);
     c[S - 1] = cinb;
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) c[j] = fma(j + 1 == S - 1 ? mulLB : bmM, c[j + 1], a[j + 1]);
@@ -404,8 +415,15 @@ fdcn_march(KArgs A) {
 #pragma unroll
       for (int i = M - 1; i >= 0; --i) {
         const int k = j * M + i;
-        y = fma(k == NPT - 1 ? glast : bm, y, V[k]);
-        V[k] = y;
+        const double wk = (i == 0 && j > 0) ? wbot[j] : R(k);
+        // y_k = mul*y_{k+1} + w_k written over V[k] (whose value, w_{k+1},
+        // was read one node earlier): the "+v" tie pins y_k to V[k]'s
+        // register so the vector stays in one register set.
+        if (k == NPT - 1)
+          asm("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "v"(glast), "v"(y), "v"(wk));
+        else
+          asm("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "s"(bm), "v"(y), "v"(wk));
+        y = V[k];
       }
     }
   };
@@ -427,7 +445,7 @@ fdcn_march(KArgs A) {
   auto build_sm = [&](const Phase& p, int tab) __attribute__((always_inline)) -> double {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) V[k] = 0.0;
-    if (t == 0) V[0] = p.inv_r;
+    X = (t == 0) ? p.inv_r : 0.0;  // e0 / r in the shifted layout
     solve(p);
     if (t < lz) {
 #pragma unroll
@@ -529,39 +547,54 @@ fdcn_march(KArgs A) {
     if (!active) { left = 0.0; right = 0.0; }
     if (shrt) V[NPT - 1] = right;
     {
-      // r_k = fma(bl, V_{k-1}, fma(bc, V_k, bu V_{k+1})) (+ dt/r lambda_k), in
-      // place: the old V_k is saved for node k+1 before it is overwritten.
-      // Written as asm so the compiler cannot evaluate all rhs values ahead
-      // of the stores (which doubles the live state and the VGPR count).
-      double prev = left;
+      // r_k = B_L V_{k-1} + B_C V_k + B_U V_{k+1} (+ mu_k), all over r: the
+      // reference's stencil (…pricer.py:531-534, …equity.py:686-691) with
+      // FMAs, evaluated left to right.  In place and SHIFTED: r_k overwrites
+      // V_{k-1} (its last reader), r_0 goes to X, so no old value needs
+      // saving.  asm keeps the compiler from evaluating every r_k before the
+      // first store (which would keep two copies of the vector live).
+      if constexpr (IT) {
+        asm volatile(
+            "v_mul_f64 %0, %4, %1\n\t"
+            "v_fma_f64 %0, %5, %2, %0\n\t"
+            "v_fma_f64 %0, %6, %3, %0\n\t"
+            "v_fma_f64 %0, %7, %8, %0"
+            : "=&v"(X)
+            : "v"(left), "v"(V[0]), "v"(V[1]), "s"(ph.bl), "s"(ph.bc), "s"(ph.bu),
+              "s"(ph.inv_r), "v"(MU[0]));
+      } else {
+        asm volatile(
+            "v_mul_f64 %0, %4, %1\n\t"
+            "v_fma_f64 %0, %5, %2, %0\n\t"
+            "v_fma_f64 %0, %6, %3, %0"
+            : "=&v"(X)
+            : "v"(left), "v"(V[0]), "v"(V[1]), "s"(ph.bl), "s"(ph.bc), "s"(ph.bu));
+      }
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) {
+      for (int k = 1; k < NPT; ++k) {
         const double nxt = (k < NPT - 1) ? V[k + 1] : right;
-        double saved;
         if constexpr (IT) {
           asm volatile(
-              "v_mov_b64 %1, %0\n\t"
-              "v_mul_f64 %0, %3, %2\n\t"
+              "v_mul_f64 %0, %3, %0\n\t"
               "v_fma_f64 %0, %4, %1, %0\n\t"
-              "v_fma_f64 %0, %5, %6, %0\n\t"
-              "v_fma_f64 %0, %7, %8, %0"
-              : "+v"(V[k]), "=&v"(saved)
-              : "v"(nxt), "s"(ph.bu), "s"(ph.bc), "s"(ph.bl), "v"(prev), "s"(ph.inv_r), "v"(MU[k]));
+              "v_fma_f64 %0, %5, %2, %0\n\t"
+              "v_fma_f64 %0, %6, %7, %0"
+              : "+v"(V[k - 1])
+              : "v"(V[k]), "v"(nxt), "s"(ph.bl), "s"(ph.bc), "s"(ph.bu), "s"(ph.inv_r),
+                "v"(MU[k]));
         } else {
           asm volatile(
-              "v_mov_b64 %1, %0\n\t"
-              "v_mul_f64 %0, %3, %2\n\t"
+              "v_mul_f64 %0, %3, %0\n\t"
               "v_fma_f64 %0, %4, %1, %0\n\t"
-              "v_fma_f64 %0, %5, %6, %0"
-              : "+v"(V[k]), "=&v"(saved)
-              : "v"(nxt), "s"(ph.bu), "s"(ph.bc), "s"(ph.bl), "v"(prev));
+              "v_fma_f64 %0, %5, %2, %0"
+              : "+v"(V[k - 1])
+              : "v"(V[k]), "v"(nxt), "s"(ph.bl), "s"(ph.bc), "s"(ph.bu));
         }
-        prev = saved;
       }
     }
-    if (t == 0) V[0] = fma(ph.fm, lo_new, V[0]);
-    if (t == L_act - 1) V[NPT - 1] = fma(ph.bm, hi_new, V[NPT - 1]);
-    if (shrt) V[NPT - 1] = 0.0;
+    if (t == 0) X = fma(ph.fm, lo_new, X);                                  // node 0
+    if (t == L_act - 1) V[NPT - 2] = fma(ph.bm, hi_new, V[NPT - 2]);        // node NPT-1
+    if (shrt) V[NPT - 2] = 0.0;  // the phantom node's rhs
 
     // ---- 2. tridiagonal solve ---------------------------------------------
     solve(ph);
