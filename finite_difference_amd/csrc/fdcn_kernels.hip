@@ -409,21 +409,22 @@ fdcn_march(KArgs A) {
     c[S - 1] = cinb;
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) c[j] = fma(j + 1 == S - 1 ? mulLB : bmM, c[j + 1], a[j + 1]);
+    // y_k = mul*y_{k+1} + w_k written over V[k] (whose value, w_{k+1}, was
+    // read one node earlier): the "+v" tie pins y_k to V[k]'s register so
+    // the vector stays in one register set.  The S sub-chains are issued
+    // round-robin (one asm statement per instruction, volatile to keep that
+    // order) so S independent FMAs are in flight.
 #pragma unroll
-    for (int j = 0; j < S; ++j) {
-      double y = c[j];
+    for (int i = M - 1; i >= 0; --i) {
 #pragma unroll
-      for (int i = M - 1; i >= 0; --i) {
+      for (int j = 0; j < S; ++j) {
         const int k = j * M + i;
         const double wk = (i == 0 && j > 0) ? wbot[j] : R(k);
-        // y_k = mul*y_{k+1} + w_k written over V[k] (whose value, w_{k+1},
-        // was read one node earlier): the "+v" tie pins y_k to V[k]'s
-        // register so the vector stays in one register set.
+        const double yn = (i == M - 1) ? c[j] : V[k + 1];
         if (k == NPT - 1)
-          asm("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "v"(glast), "v"(y), "v"(wk));
+          asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "v"(glast), "v"(yn), "v"(wk));
         else
-          asm("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "s"(bm), "v"(y), "v"(wk));
-        y = V[k];
+          asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "s"(bm), "v"(yn), "v"(wk));
       }
     }
   };
@@ -553,42 +554,37 @@ fdcn_march(KArgs A) {
       // V_{k-1} (its last reader), r_0 goes to X, so no old value needs
       // saving.  asm keeps the compiler from evaluating every r_k before the
       // first store (which would keep two copies of the vector live).
-      if constexpr (IT) {
-        asm volatile(
-            "v_mul_f64 %0, %4, %1\n\t"
-            "v_fma_f64 %0, %5, %2, %0\n\t"
-            "v_fma_f64 %0, %6, %3, %0\n\t"
-            "v_fma_f64 %0, %7, %8, %0"
-            : "=&v"(X)
-            : "v"(left), "v"(V[0]), "v"(V[1]), "s"(ph.bl), "s"(ph.bc), "s"(ph.bu),
-              "s"(ph.inv_r), "v"(MU[0]));
-      } else {
-        asm volatile(
-            "v_mul_f64 %0, %4, %1\n\t"
-            "v_fma_f64 %0, %5, %2, %0\n\t"
-            "v_fma_f64 %0, %6, %3, %0"
-            : "=&v"(X)
-            : "v"(left), "v"(V[0]), "v"(V[1]), "s"(ph.bl), "s"(ph.bc), "s"(ph.bu));
-      }
+      // Software-pipelined over nodes: step s issues op4 of node s-3 (IT
+      // only), op3 of node s-2, op2 of node s-1 and op1 of node s, so each
+      // node's dependent chain is spread 3-4 instructions apart and node
+      // j+1's first write to V[j] comes after the last reads of the old V[j]
+      // (op2 of node j, op3 of node j-1).  One asm statement per
+      // instruction keeps that order; the "+v" ties keep it in place.
+      //   op1: acc_j  = B_L * V_{j-1}     (acc_0 = X, acc_j = V[j-1])
+      //   op2: acc_j += B_C * V_j
+      //   op3: acc_j += B_U * V_{j+1}     (V_NPT = right)
+      //   op4: acc_j += mu_j / r          (IT)
+      constexpr int kOps = IT ? 4 : 3;
 #pragma unroll
-      for (int k = 1; k < NPT; ++k) {
-        const double nxt = (k < NPT - 1) ? V[k + 1] : right;
-        if constexpr (IT) {
-          asm volatile(
-              "v_mul_f64 %0, %3, %0\n\t"
-              "v_fma_f64 %0, %4, %1, %0\n\t"
-              "v_fma_f64 %0, %5, %2, %0\n\t"
-              "v_fma_f64 %0, %6, %7, %0"
-              : "+v"(V[k - 1])
-              : "v"(V[k]), "v"(nxt), "s"(ph.bl), "s"(ph.bc), "s"(ph.bu), "s"(ph.inv_r),
-                "v"(MU[k]));
-        } else {
-          asm volatile(
-              "v_mul_f64 %0, %3, %0\n\t"
-              "v_fma_f64 %0, %4, %1, %0\n\t"
-              "v_fma_f64 %0, %5, %2, %0"
-              : "+v"(V[k - 1])
-              : "v"(V[k]), "v"(nxt), "s"(ph.bl), "s"(ph.bc), "s"(ph.bu));
+      for (int st = 0; st < NPT + kOps - 1; ++st) {
+#pragma unroll
+        for (int op = kOps; op >= 1; --op) {
+          const int j = st - (op - 1);
+          if (j < 0 || j >= NPT) continue;
+          double& acc = (j == 0) ? X : V[j - 1];
+          if (op == 1) {
+            if (j == 0)
+              asm volatile("v_mul_f64 %0, %1, %2" : "=v"(X) : "s"(ph.bl), "v"(left));
+            else
+              asm volatile("v_mul_f64 %0, %1, %0" : "+v"(acc) : "s"(ph.bl));
+          } else if (op == 2) {
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(acc) : "s"(ph.bc), "v"(V[j]));
+          } else if (op == 3) {
+            const double nxt = (j < NPT - 1) ? V[j + 1] : right;
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(acc) : "s"(ph.bu), "v"(nxt));
+          } else {
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(acc) : "s"(ph.inv_r), "v"(MU[j]));
+          }
         }
       }
     }
@@ -621,22 +617,41 @@ fdcn_march(KArgs A) {
       // fd_american_equity.py:704-717; max() differs from the reference's
       // compare-select only in the sign of an exact zero
       const int off = opaque(kPhiLds ? t : s_t + 1);
+      // fd_american_equity.py:704-717 with mu = dt*lambda:
+      //   v~ = V - mu;  mu' = max(phi - v~, 0);  V' = max(phi, v~)
+      // (= dt * max(lambda + (phi - V)/dt, 0) and max(phi, V - dt lambda) in
+      // exact arithmetic).  In place, four nodes per block with the
+      // instructions interleaved so the dependent chains overlap.
+      static_assert(NPT % 4 == 0, "IT variants need NPT divisible by 4");
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) {
-        const int node = s_t + 1 + k;
-        const double pk = kPhiLds ? phit[off + k * L]
-                                  : ((active && node <= n_int) ? pin[off + k] : 0.0);
-        // fd_american_equity.py:704-717 with mu = dt*lambda:
-        //   v~ = V - mu;  mu' = max(phi - v~, 0);  V' = max(phi, v~)
-        // (= dt * max(lambda + (phi - V)/dt, 0) and max(phi, V - dt lambda)
-        // in exact arithmetic; 4 instructions, in place)
+      for (int k = 0; k < NPT; k += 4) {
+        double pk[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int node = s_t + 1 + k + i;
+          pk[i] = kPhiLds ? phit[off + (k + i) * L]
+                          : ((active && node <= n_int) ? pin[off + k + i] : 0.0);
+        }
         asm volatile(
-            "v_add_f64 %0, %0, -%1\n\t"
-            "v_add_f64 %1, %2, -%0\n\t"
-            "v_max_f64 %1, %1, 0\n\t"
-            "v_max_f64 %0, %2, %0"
-            : "+v"(V[k]), "+v"(MU[k])
-            : "v"(pk));
+            "v_add_f64 %0, %0, -%4\n\t"
+            "v_add_f64 %1, %1, -%5\n\t"
+            "v_add_f64 %2, %2, -%6\n\t"
+            "v_add_f64 %3, %3, -%7\n\t"
+            "v_add_f64 %4, %8, -%0\n\t"
+            "v_add_f64 %5, %9, -%1\n\t"
+            "v_add_f64 %6, %10, -%2\n\t"
+            "v_add_f64 %7, %11, -%3\n\t"
+            "v_max_f64 %0, %8, %0\n\t"
+            "v_max_f64 %1, %9, %1\n\t"
+            "v_max_f64 %2, %10, %2\n\t"
+            "v_max_f64 %3, %11, %3\n\t"
+            "v_max_f64 %4, %4, 0\n\t"
+            "v_max_f64 %5, %5, 0\n\t"
+            "v_max_f64 %6, %6, 0\n\t"
+            "v_max_f64 %7, %7, 0"
+            : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(MU[k]),
+              "+v"(MU[k + 1]), "+v"(MU[k + 2]), "+v"(MU[k + 3])
+            : "v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]));
       }
       if (shrt) MU[NPT - 1] = 0.0;
     }
