@@ -80,6 +80,28 @@ __device__ __forceinline__ int opaque(int i) {
   return i;
 }
 
+// Diagnostic build only (-DFDCN_STAMPS): per-phase cycle counters of the time
+// loop, summed over waves into fdcn_stamps[] (read by fdcn_debug_stamps).  A
+// stamp is s_memtime + lgkmcnt(0) fenced by sched_barriers; it forbids overlap
+// across phases, so read the SHARES, never the diagnostic build's run time.
+#ifdef FDCN_STAMPS
+constexpr int kNumStamps = 9;
+__device__ unsigned long long fdcn_stamps[kNumStamps + 1];
+#define FDCN_STAMP(acc, prev, i)                                                  \
+  do {                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    unsigned long long now_;                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now_)::"memory");  \
+    acc[i] += now_ - prev;                                                       \
+    prev = now_;                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+  } while (0)
+#else
+#define FDCN_STAMP(acc, prev, i) \
+  do {                           \
+  } while (0)
+#endif
+
 __device__ __forceinline__ double shfl_up1(double x, int d) { return __shfl_up(x, (unsigned)d, 64); }
 __device__ __forceinline__ double shfl_dn1(double x, int d) { return __shfl_down(x, (unsigned)d, 64); }
 
@@ -310,6 +332,11 @@ fdcn_march(KArgs A) {
     }
   };
 
+#ifdef FDCN_STAMPS
+  unsigned long long st_acc[kNumStamps] = {0};
+  unsigned long long st_prev = 0;
+  bool st_on = false;  // count only inside the time loop
+#endif
   // Forward + backward sweeps.  Input: rhs/r in the SHIFTED layout left by
   // the in-place RHS (node 0 in X, node k >= 1 in V[k-1]); output: the
   // solution in the natural layout (node k in V[k]).  The forward pass works
@@ -334,6 +361,7 @@ fdcn_march(KArgs A) {
     double e = a[0];
 #pragma unroll
     for (int j = 1; j < S; ++j) e = fma(j == S - 1 ? mulLF : fmM, e, a[j]);
+    FDCN_STAMP(st_acc, st_prev, 2);
     double b = active ? e : 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -352,6 +380,7 @@ fdcn_march(KArgs A) {
     double cin = shfl_up1(b, 1);
     if (lane == 0) cin = cw;
     if (!active) cin = 0.0;
+    FDCN_STAMP(st_acc, st_prev, 3);
     // forward pass 2: carries into every sub-chain, then S chains in parallel
     double c[S];
     c[0] = cin;
@@ -367,6 +396,7 @@ fdcn_march(KArgs A) {
         R(k) = (k == NPT - 1 && shrt) ? 0.0 : w;
       }
     }
+    FDCN_STAMP(st_acc, st_prev, 4);
     // backward pass 1: zero-carry start value of every sub-chain
 #pragma unroll
     for (int j = 0; j < S; ++j) {
@@ -383,6 +413,7 @@ fdcn_march(KArgs A) {
     e = a[S - 1];
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) e = fma(bmM, e, a[j]);
+    FDCN_STAMP(st_acc, st_prev, 5);
     double cb = active ? e : 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -401,6 +432,7 @@ fdcn_march(KArgs A) {
     double cinb = shfl_dn1(cb, 1);
     if (lane == 63) cinb = cwb;
     if (!active) cinb = 0.0;
+    FDCN_STAMP(st_acc, st_prev, 6);
     // backward pass 2 (unshifting).  Sub-chain j-1 writes V[jM-1], which
     // holds sub-chain j's last input (node jM): read those first.
     double wbot[S];
@@ -520,6 +552,12 @@ fdcn_march(KArgs A) {
 
   double2 bnd_cur = make_double2(0.0, 0.0);
   double2 bnd_nxt = bnd[lane];  // steps 0..63
+#ifdef FDCN_STAMPS
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+  for (int i = 0; i < kNumStamps; ++i) st_acc[i] = 0;
+  st_on = true;
+  (void)st_on;
+#endif
   for (int m = 0; m < A.n_time; ++m) {
     if (m == A.n_ranna && use_r) {  // Rannacher -> Crank-Nicolson
       ph = make_phase(0.5, dt, ca, cc, cbc);
@@ -534,6 +572,7 @@ fdcn_march(KArgs A) {
     const double lo_new = read_lane(bnd_cur.x, m & 63);
     const double hi_new = read_lane(bnd_cur.y, m & 63);
 
+    FDCN_STAMP(st_acc, st_prev, 0);
     // ---- 1. rhs/r ----------------------------------------------------------
     if constexpr (W > 1) __syncthreads();  // halos of the previous step
     const double last_real = shrt ? V[NPT - 2] : V[NPT - 1];
@@ -592,67 +631,99 @@ fdcn_march(KArgs A) {
     if (t == L_act - 1) V[NPT - 2] = fma(ph.bm, hi_new, V[NPT - 2]);        // node NPT-1
     if (shrt) V[NPT - 2] = 0.0;  // the phantom node's rhs
 
+    FDCN_STAMP(st_acc, st_prev, 1);
     // ---- 2. tridiagonal solve ---------------------------------------------
     solve(ph);
-    // Sherman-Morrison: x = y - (k y0 / (1 + k z0)) z over the first lz lanes.
-    // Branch-free (a zero multiplier outside): a divergent branch here makes
-    // the compiler keep two copies of V live.
-    if ((W == 1) || (lz > 64) || (wave == 0)) {
+    FDCN_STAMP(st_acc, st_prev, 7);
+    // Sherman-Morrison: x = y - (k y0 / (1 + k z0)) z over the first lz lanes
+    // (lanes >= lz use g = 0 and read row lz-1, one broadcast address), fused
+    // with the Ikonen-Toivanen update for IT.  Both tables are read from LDS
+    // one 4-node group ahead of their use, so the LDS latency overlaps the
+    // previous group's arithmetic.
+    static_assert(NPT % 4 == 0, "variants need NPT divisible by 4");
+    const bool do_sm = (W == 1) || (lz > 64) || (wave == 0);
+    double g = 0.0;
+    int zoff = 0;
+    if (do_sm) {
       double y0;
       if constexpr (W == 1) {
         y0 = read_lane(V[0], 0);
       } else {
         y0 = (lz > 64) ? bcast_first(V[0]) : read_lane(V[0], 0);
       }
-      const double g = (t < lz) ? -(smc * y0) : 0.0;
-      // lane-major rows (stride NPT+1: bank-spread, immediate offsets);
-      // lanes >= lz read row lz-1 with g = 0
-      const int off = opaque((tab * lz + (t < lz ? t : lz - 1)) * (NPT + 1));
-#pragma unroll
-      for (int k = 0; k < NPT; ++k) V[k] = fma(g, ztab[off + k], V[k]);
+      g = (t < lz) ? -(smc * y0) : 0.0;
+      // lane-major rows, stride NPT+1: bank-spread, immediate offsets
+      zoff = opaque((tab * lz + (t < lz ? t : lz - 1)) * (NPT + 1));
     }
-
+    FDCN_STAMP(st_acc, st_prev, 8);
     // ---- 3. early exercise / boundaries / knock-out ------------------------
-    if constexpr (IT) {
-      // fd_american_equity.py:704-717; max() differs from the reference's
-      // compare-select only in the sign of an exact zero
-      const int off = opaque(kPhiLds ? t : s_t + 1);
-      // fd_american_equity.py:704-717 with mu = dt*lambda:
-      //   v~ = V - mu;  mu' = max(phi - v~, 0);  V' = max(phi, v~)
-      // (= dt * max(lambda + (phi - V)/dt, 0) and max(phi, V - dt lambda) in
-      // exact arithmetic).  In place, four nodes per block with the
-      // instructions interleaved so the dependent chains overlap.
-      static_assert(NPT % 4 == 0, "IT variants need NPT divisible by 4");
+    {
+      const int poff = opaque(kPhiLds ? t : s_t + 1);
+      auto phi_at = [&](int k) -> double {
+        const int node = s_t + 1 + k;
+        return kPhiLds ? phit[poff + k * L]
+                       : ((active && node <= n_int) ? pin[poff + k] : 0.0);
+      };
+      double zn[4], pn[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        zn[i] = do_sm ? ztab[zoff + i] : 0.0;
+        if constexpr (IT) pn[i] = phi_at(i);
+      }
 #pragma unroll
       for (int k = 0; k < NPT; k += 4) {
-        double pk[4];
+        double zk[4], pk[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int node = s_t + 1 + k + i;
-          pk[i] = kPhiLds ? phit[off + (k + i) * L]
-                          : ((active && node <= n_int) ? pin[off + k + i] : 0.0);
+          zk[i] = zn[i];
+          pk[i] = pn[i];
         }
-        asm volatile(
-            "v_add_f64 %0, %0, -%4\n\t"
-            "v_add_f64 %1, %1, -%5\n\t"
-            "v_add_f64 %2, %2, -%6\n\t"
-            "v_add_f64 %3, %3, -%7\n\t"
-            "v_add_f64 %4, %8, -%0\n\t"
-            "v_add_f64 %5, %9, -%1\n\t"
-            "v_add_f64 %6, %10, -%2\n\t"
-            "v_add_f64 %7, %11, -%3\n\t"
-            "v_max_f64 %0, %8, %0\n\t"
-            "v_max_f64 %1, %9, %1\n\t"
-            "v_max_f64 %2, %10, %2\n\t"
-            "v_max_f64 %3, %11, %3\n\t"
-            "v_max_f64 %4, %4, 0\n\t"
-            "v_max_f64 %5, %5, 0\n\t"
-            "v_max_f64 %6, %6, 0\n\t"
-            "v_max_f64 %7, %7, 0"
-            : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(MU[k]),
-              "+v"(MU[k + 1]), "+v"(MU[k + 2]), "+v"(MU[k + 3])
-            : "v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]));
+        if (k + 4 < NPT) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            zn[i] = do_sm ? ztab[zoff + k + 4 + i] : 0.0;
+            if constexpr (IT) pn[i] = phi_at(k + 4 + i);
+          }
+        }
+        if constexpr (!IT) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) V[k + i] = fma(g, zk[i], V[k + i]);
+        } else {
+          // x = y + g z, then fd_american_equity.py:704-717 with mu = dt*lambda:
+          //   v~ = x - mu;  mu' = max(phi - v~, 0);  V' = max(phi, v~)
+          // (= dt * max(lambda + (phi - x)/dt, 0) and max(phi, x - dt lambda)
+          // in exact arithmetic; the reference's compare-select can differ
+          // only in the sign of an exact zero).  In place, the four nodes'
+          // dependent chains interleaved.
+          asm volatile(
+              "v_fma_f64 %0, %12, %13, %0\n\t"
+              "v_fma_f64 %1, %12, %14, %1\n\t"
+              "v_fma_f64 %2, %12, %15, %2\n\t"
+              "v_fma_f64 %3, %12, %16, %3\n\t"
+              "v_add_f64 %0, %0, -%4\n\t"
+              "v_add_f64 %1, %1, -%5\n\t"
+              "v_add_f64 %2, %2, -%6\n\t"
+              "v_add_f64 %3, %3, -%7\n\t"
+              "v_add_f64 %4, %8, -%0\n\t"
+              "v_add_f64 %5, %9, -%1\n\t"
+              "v_add_f64 %6, %10, -%2\n\t"
+              "v_add_f64 %7, %11, -%3\n\t"
+              "v_max_f64 %0, %8, %0\n\t"
+              "v_max_f64 %1, %9, %1\n\t"
+              "v_max_f64 %2, %10, %2\n\t"
+              "v_max_f64 %3, %11, %3\n\t"
+              "v_max_f64 %4, %4, 0\n\t"
+              "v_max_f64 %5, %5, 0\n\t"
+              "v_max_f64 %6, %6, 0\n\t"
+              "v_max_f64 %7, %7, 0"
+              : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(MU[k]),
+                "+v"(MU[k + 1]), "+v"(MU[k + 2]), "+v"(MU[k + 3])
+              : "v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]), "v"(g), "v"(zk[0]),
+                "v"(zk[1]), "v"(zk[2]), "v"(zk[3]));
+        }
       }
+    }
+    if constexpr (IT) {
       if (shrt) MU[NPT - 1] = 0.0;
     }
     V0 = lo_new;
@@ -677,6 +748,13 @@ fdcn_march(KArgs A) {
     }
   }
 
+#ifdef FDCN_STAMPS
+  FDCN_STAMP(st_acc, st_prev, 0);  // IT/KO tail of the last step -> bucket 0
+  if (lane == 0 && wave == 0) {
+    for (int i = 0; i < kNumStamps; ++i) atomicAdd(&fdcn_stamps[i], st_acc[i]);
+    atomicAdd(&fdcn_stamps[kNumStamps], 1ull);
+  }
+#endif
   // ---- store ---------------------------------------------------------------
   double* vout = A.v_out + (size_t)scen * n_nodes;
   const double poison = overflow ? __longlong_as_double(0x7ff8000000000000ll) : 0.0;
@@ -1034,5 +1112,19 @@ int fdcn_device_count(void) {
 }
 
 int fdcn_abi_version(void) { return FDCN_ABI_VERSION; }
+
+#ifdef FDCN_STAMPS
+// Diagnostic build only: copy (and with reset != 0, zero) the per-phase cycle
+// sums; out[kNumStamps] is the number of waves that contributed.
+int fdcn_debug_stamps(unsigned long long* out, int reset) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(fdcn_stamps), sizeof(fdcn_stamps)));
+  if (reset) {
+    unsigned long long z[kNumStamps + 1] = {0};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(fdcn_stamps), z, sizeof(z)));
+  }
+  return kNumStamps;
+}
+#endif
 
 }  // extern "C"
