@@ -10,5 +10,5 @@ rc=$?; echo "tests rc=$rc" >> gpurun_out/${TAG}_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
 if [ -f finite_difference_amd/_lib/libfdcn_stamps.so ]; then
-  timeout -k 10 300 python tools/stamps.py 4096 it > gpurun_out/${TAG}_stamps.json 2>> gpurun_out/${TAG}_bench.err || exit $?
+  timeout -k 10 300 python tools/stamps.py american > gpurun_out/${TAG}_stamps.json 2>> gpurun_out/${TAG}_bench.err || exit $?
 fi

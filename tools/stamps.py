@@ -21,10 +21,11 @@ NAMES = ["IT/KO + loop top", "halo + RHS", "fwd pass 1", "fwd scan", "fwd pass 2
 def main():
     import numpy as np
     import bench
-    B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-    it = (sys.argv[2] if len(sys.argv) > 2 else "it") == "it"
+    wl = sys.argv[1] if len(sys.argv) > 1 else "american"
+    builder, ns, nt, it, _ = bench.WORKLOADS[wl]
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else bench.DEFAULT_BATCH[wl]
     L = ctypes.CDLL(os.path.join(ROOT, "finite_difference_amd", "_lib", "libfdcn_stamps.so"))
-    g = bench.build_workload(B, 2048, 4096, seed=0)
+    g = builder(B, ns, nt, seed=0)
     D, I = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
     out = np.empty_like(g.v_init)
     st = (ctypes.c_ulonglong * 10)()
@@ -34,11 +35,12 @@ def main():
                              g.iparams.ctypes.data_as(I), g.v_init.ctypes.data_as(D),
                              g.payoff.ctypes.data_as(D), out.ctypes.data_as(D))
     else:
-        ms = np.zeros(1, np.int32)
-        mr = np.zeros(1)
+        ms = g.mon_step if len(g.mon_step) else np.zeros(1, np.int32)
+        mr = g.mon_rebate if len(g.mon_rebate) else np.zeros(1)
         rc = L.fdcn_cn_batch(g.B, g.n_nodes, g.n_time, g.n_ranna, g.params.ctypes.data_as(D),
-                             g.iparams.ctypes.data_as(I), g.v_init.ctypes.data_as(D), 0,
-                             ms.ctypes.data_as(I), mr.ctypes.data_as(D), out.ctypes.data_as(D))
+                             g.iparams.ctypes.data_as(I), g.v_init.ctypes.data_as(D),
+                             len(g.mon_step), ms.ctypes.data_as(I), mr.ctypes.data_as(D),
+                             out.ctypes.data_as(D))
     assert rc == 0, rc
     L.fdcn_debug_stamps(st, 0)
     vals = [st[i] for i in range(9)]
