@@ -176,6 +176,29 @@ __device__ __forceinline__ double pow_n(double x, int n) {
   return r;
 }
 
+// (lane, slot) of interior index i (0-based) under the short-lane layout:
+// the first Ls lanes hold NPT-1 nodes, the rest NPT.
+template <int NPT>
+__device__ __forceinline__ void lane_slot(int i, int Ls, int& lane, int& slot) {
+  const int split = Ls * (NPT - 1);
+  if (i < split) {
+    lane = i / (NPT - 1);
+    slot = i - lane * (NPT - 1);
+  } else {
+    lane = Ls + (i - split) / NPT;
+    slot = (i - split) - (lane - Ls) * NPT;
+  }
+}
+
+// Knock-out lane masks of one wave, as wave-uniform 64-bit values: slot k of
+// the lanes in `full` is knocked out for every k; lane `part` (if any) for k
+// in [k0, k1].  The per-slot mask is then two scalar selects and an OR, and
+// the projection two v_cndmask per slot with an SGPR mask.
+struct KoMask {
+  unsigned long long full, part;
+  int k0, k1;
+};
+
 // ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
@@ -529,9 +552,49 @@ fdcn_march(KArgs A) {
   }
   const int ko_lo = uni_i(I[FDCN_I_KO_LO]);
   const int ko_hi = uni_i(I[FDCN_I_KO_HI]);
+  // knock-out masks of this wave (interior nodes j <= ko_lo or j >= ko_hi),
+  // computed once: lanes are ordered by node, so the knocked-out lanes of
+  // each side are a contiguous run plus at most one partial lane
+  KoMask kml{0ull, 0ull, 0, -1}, kmh{0ull, 0ull, 0, -1};
+  if constexpr (!IT) {
+    const unsigned long long act =
+        __builtin_amdgcn_read_exec() & (unsigned long long)__ballot(active);
+    const int base = wave * 64;
+    if (ko_lo >= 1) {  // interior indices 0 .. ko_lo-1 are out
+      int tl, sl;
+      if (ko_lo >= n_int) { tl = L_act; sl = 0; }
+      else lane_slot<NPT>(ko_lo - 1, L_short, tl, sl);
+      // lanes < tl fully out; lane tl out for slots <= sl
+      const int rl = tl - base;
+      kml.full = rl <= 0 ? 0ull : (rl >= 64 ? ~0ull : ((1ull << rl) - 1ull));
+      kml.full &= act;
+      if (ko_lo < n_int && rl >= 0 && rl < 64) { kml.part = 1ull << rl; kml.k0 = 0; kml.k1 = sl; }
+    }
+    if (ko_hi <= n_int) {  // interior indices ko_hi-1 .. n_int-1 are out
+      int th, sh;
+      if (ko_hi <= 1) { th = 0; sh = 0; }
+      else lane_slot<NPT>(ko_hi - 1, L_short, th, sh);
+      // lane th out for slots >= sh; lanes > th fully out
+      const int rh = th - base;
+      kmh.full = rh >= 63 ? 0ull : (rh < 0 ? ~0ull : ~((2ull << rh) - 1ull));
+      kmh.full &= act;
+      if (rh >= 0 && rh < 64) { kmh.part = 1ull << rh; kmh.k0 = sh; kmh.k1 = NPT - 1; }
+    }
+  }
   int mpos = uni_i(I[FDCN_I_MON_START]);
   const int mend = mpos + uni_i(I[FDCN_I_MON_COUNT]);
-  int next_mon = (mpos < mend) ? uni_i(A.mon_step[mpos]) : 0x7fffffff;
+  // monitor entry mpos (step, rebate) and the next one, loaded a monitor
+  // step ahead of their use so the scalar-load latency is off the step
+  int next_mon = 0x7fffffff, pf_mon = 0x7fffffff;
+  double cur_reb = 0.0, pf_reb = 0.0;
+  if (!IT && mpos < mend) {
+    next_mon = uni_i(A.mon_step[mpos]);
+    cur_reb = uni(A.mon_rebate[mpos]);
+    if (mpos + 1 < mend) {
+      pf_mon = uni_i(A.mon_step[mpos + 1]);
+      pf_reb = uni(A.mon_rebate[mpos + 1]);
+    }
+  }
 
   if constexpr (W > 1) {
     if (lane == 0) xch[Xch<W>::kFirst + wave] = V[0];
@@ -552,6 +615,11 @@ fdcn_march(KArgs A) {
 
   double2 bnd_cur = make_double2(0.0, 0.0);
   double2 bnd_nxt = bnd[lane];  // steps 0..63
+  double halo_l = 0.0, halo_r = 0.0;
+  if constexpr (W == 1) {
+    halo_l = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
+    halo_r = shfl_dn1(V[0], 1);
+  }
 #ifdef FDCN_STAMPS
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
   for (int i = 0; i < kNumStamps; ++i) st_acc[i] = 0;
@@ -575,10 +643,12 @@ fdcn_march(KArgs A) {
     FDCN_STAMP(st_acc, st_prev, 0);
     // ---- 1. rhs/r ----------------------------------------------------------
     if constexpr (W > 1) __syncthreads();  // halos of the previous step
-    const double last_real = shrt ? V[NPT - 2] : V[NPT - 1];
-    double left = shfl_up1(last_real, 1);
-    double right = shfl_dn1(V[0], 1);
+    // neighbours' edge values: shuffled at the end of the previous step (W=1)
+    // so their latency overlaps the tail of that step
+    double left = halo_l, right = halo_r;
     if constexpr (W > 1) {
+      left = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
+      right = shfl_dn1(V[0], 1);
       if (lane == 0 && wave > 0) left = xch[Xch<W>::kLast + wave - 1];
       if (lane == 63 && wave < W - 1) right = xch[Xch<W>::kFirst + wave + 1];
     }
@@ -611,11 +681,19 @@ fdcn_march(KArgs A) {
           const int j = st - (op - 1);
           if (j < 0 || j >= NPT) continue;
           double& acc = (j == 0) ? X : V[j - 1];
+          if (j == 0) {
+            // node 0 takes the left neighbour last: r_0 = (B_C V_0 + B_U V_1)
+            // + B_L left, so the halo shuffle has the whole RHS to land
+            if (op == 1)
+              asm volatile("v_mul_f64 %0, %1, %2" : "=v"(X) : "s"(ph.bc), "v"(V[0]));
+            else if (op == 2)
+              asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(X) : "s"(ph.bu), "v"(V[1]));
+            else if (op == 4)
+              asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(X) : "s"(ph.inv_r), "v"(MU[0]));
+            continue;
+          }
           if (op == 1) {
-            if (j == 0)
-              asm volatile("v_mul_f64 %0, %1, %2" : "=v"(X) : "s"(ph.bl), "v"(left));
-            else
-              asm volatile("v_mul_f64 %0, %1, %0" : "+v"(acc) : "s"(ph.bl));
+            asm volatile("v_mul_f64 %0, %1, %0" : "+v"(acc) : "s"(ph.bl));
           } else if (op == 2) {
             asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(acc) : "s"(ph.bc), "v"(V[j]));
           } else if (op == 3) {
@@ -627,6 +705,7 @@ fdcn_march(KArgs A) {
         }
       }
     }
+    asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(X) : "s"(ph.bl), "v"(left));
     if (t == 0) X = fma(ph.fm, lo_new, X);                                  // node 0
     if (t == L_act - 1) V[NPT - 2] = fma(ph.bm, hi_new, V[NPT - 2]);        // node NPT-1
     if (shrt) V[NPT - 2] = 0.0;  // the phantom node's rhs
@@ -728,23 +807,48 @@ fdcn_march(KArgs A) {
     }
     V0 = lo_new;
     VN = hi_new;
-    if (!IT && m + 1 == next_mon) {  // knock-out projection (uniform branch, per-node select)
-      const double reb = uni(A.mon_rebate[mpos]);
-      // opaque: keep the per-slot masks inside this rare branch (hoisted out
-      // of the loop they would pin 2*NPT SGPRs for the whole march)
-      const int klo = opaque(active ? ko_lo - s_t - 1 : -1);       // slots k <= klo are out
-      const int khi = opaque(active ? ko_hi - s_t - 1 : NPT + 1);  // slots k >= khi are out
+    if (!IT && m + 1 == next_mon) {  // knock-out projection (uniform branch)
+      const double reb = cur_reb;
+      double rebv = reb;  // VGPR copy: v_cndmask takes the mask as its SGPR operand
+      asm volatile("" : "+v"(rebv));
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) V[k] = (k <= klo || k >= khi) ? reb : V[k];
+      for (int k = 0; k < NPT; ++k) {
+        const unsigned long long mk = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) |
+                                      kmh.full | ((k >= kmh.k0 && k <= kmh.k1) ? kmh.part : 0ull);
+        unsigned lo = (unsigned)__double_as_longlong(V[k]);
+        unsigned hi = (unsigned)(__double_as_longlong(V[k]) >> 32);
+        const unsigned rlo = (unsigned)__double_as_longlong(rebv);
+        const unsigned rhi = (unsigned)(__double_as_longlong(rebv) >> 32);
+        asm volatile("v_cndmask_b32 %0, %0, %2, %4\n\t"
+                     "v_cndmask_b32 %1, %1, %3, %4"
+                     : "+v"(lo), "+v"(hi)
+                     : "v"(rlo), "v"(rhi), "s"(mk));
+        V[k] = __longlong_as_double(((long long)hi << 32) | lo);
+      }
       if (0 <= ko_lo) V0 = reb;
       if (n_nodes - 1 >= ko_hi) VN = reb;
+      // advance to the prefetched entry; request the one after it
       ++mpos;
-      while (mpos < mend && uni_i(A.mon_step[mpos]) <= m + 1) ++mpos;
-      next_mon = (mpos < mend) ? uni_i(A.mon_step[mpos]) : 0x7fffffff;
+      next_mon = mpos < mend ? pf_mon : 0x7fffffff;
+      cur_reb = pf_reb;
+      if (mpos + 1 < mend) {
+        pf_mon = uni_i(A.mon_step[mpos + 1]);
+        pf_reb = uni(A.mon_rebate[mpos + 1]);
+      }
+      if (next_mon <= m + 1) {  // entries not strictly increasing: skip (slow path)
+        while (mpos < mend && uni_i(A.mon_step[mpos]) <= m + 1) ++mpos;
+        next_mon = (mpos < mend) ? uni_i(A.mon_step[mpos]) : 0x7fffffff;
+        cur_reb = (mpos < mend) ? uni(A.mon_rebate[mpos]) : 0.0;
+        pf_mon = (mpos + 1 < mend) ? uni_i(A.mon_step[mpos + 1]) : 0x7fffffff;
+        pf_reb = (mpos + 1 < mend) ? uni(A.mon_rebate[mpos + 1]) : 0.0;
+      }
     }
     if constexpr (W > 1) {
       if (lane == 0) xch[Xch<W>::kFirst + wave] = V[0];
       if (lane == 63) xch[Xch<W>::kLast + wave] = shrt ? V[NPT - 2] : V[NPT - 1];
+    } else {
+      halo_l = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
+      halo_r = shfl_dn1(V[0], 1);
     }
   }
 
