@@ -223,7 +223,7 @@ def main():
     g = builder(B, n_space, n_time, seed=rank)
     t_build = time.perf_counter() - t_build
     k_cap = capi.sm_extent(g.n_nodes, g.n_time, g.n_ranna, g.params)
-    plan = capi.plan(g.n_nodes, is_it, k_cap, n_time=g.n_time)
+    plan = capi.plan(g.n_nodes, is_it, k_cap, n_time=g.n_time, B=g.B)
 
     P = torch.from_numpy(g.params).to(dev)
     I = torch.from_numpy(g.iparams).to(dev)

@@ -26,7 +26,7 @@ P_HI_C0, P_HI_E0, P_HI_C1, P_HI_E1 = 9, 10, 11, 12
 NPARAM = 13
 I_LO_FORM, I_HI_FORM, I_KO_LO, I_KO_HI, I_MON_START, I_MON_COUNT, I_TAU_MODE = range(7)
 NIPARAM = 7
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batch_dev",
             "fdcn_plan", "fdcn_sm_extent", "fdcn_last_error", "fdcn_device_count",
@@ -66,7 +66,7 @@ def lib() -> ctypes.CDLL:
             L.fdcn_it_batch_dev.restype = _I
             L.fdcn_it_batch_dev.argtypes = [_I, _I, _I, _I, _V, _V, _V, _V, _V, _I, _V, _V]
             L.fdcn_plan.restype = _I
-            L.fdcn_plan.argtypes = [_I, _I, _I, _I, _PI, _PI, _PI, _PI,
+            L.fdcn_plan.argtypes = [_I, _I, _I, _I, _I, _PI, _PI, _PI, _PI,
                                     ctypes.POINTER(ctypes.c_int64)]
             L.fdcn_sm_extent.restype = _I
             L.fdcn_sm_extent.argtypes = [_I, _I, _I, _I, _PD]
@@ -105,10 +105,11 @@ def _i32(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.int32)
 
 
-def plan(n_nodes: int, it_mode: bool, k_cap: int = 0, n_time: int = 1) -> dict:
+def plan(n_nodes: int, it_mode: bool, k_cap: int = 0, n_time: int = 1, B: int = 1 << 20) -> dict:
+    """Launch geometry for B scenarios (the default B is a large batch)."""
     w, npt, spb, lds = (ctypes.c_int32() for _ in range(4))
     ws = ctypes.c_int64()
-    _check(lib().fdcn_plan(n_nodes, n_time, 1 if it_mode else 0, k_cap, ctypes.byref(w),
+    _check(lib().fdcn_plan(B, n_nodes, n_time, 1 if it_mode else 0, k_cap, ctypes.byref(w),
                            ctypes.byref(npt), ctypes.byref(spb), ctypes.byref(lds),
                            ctypes.byref(ws)))
     return dict(waves=w.value, npt=npt.value, scen_per_block=spb.value, lds_bytes=lds.value,

@@ -42,6 +42,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -102,8 +103,29 @@ __device__ unsigned long long fdcn_stamps[kNumStamps + 1];
   } while (0)
 #endif
 
-__device__ __forceinline__ double shfl_up1(double x, int d) { return __shfl_up(x, (unsigned)d, 64); }
-__device__ __forceinline__ double shfl_dn1(double x, int d) { return __shfl_down(x, (unsigned)d, 64); }
+// Cross-lane moves.  Shifts by one lane use the GFX9 wavefront DPP shifts
+// (wave_shr:1 / wave_shl:1: two VALU moves, no LDS round trip), by two lanes
+// two of them; longer shifts go through ds_bpermute.  Lanes without a source
+// receive 0 (DPP) or their own value (bpermute); every caller masks them.
+template <int CTRL>
+__device__ __forceinline__ double dpp_move(double x) {
+  const unsigned long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffull), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1
+constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1
+__device__ __forceinline__ double shfl_up1(double x, int d) {
+  if (d == 1) return dpp_move<kDppWaveShr1>(x);
+  if (d == 2) return dpp_move<kDppWaveShr1>(dpp_move<kDppWaveShr1>(x));
+  return __shfl_up(x, (unsigned)d, 64);
+}
+__device__ __forceinline__ double shfl_dn1(double x, int d) {
+  if (d == 1) return dpp_move<kDppWaveShl1>(x);
+  if (d == 2) return dpp_move<kDppWaveShl1>(dpp_move<kDppWaveShl1>(x));
+  return __shfl_down(x, (unsigned)d, 64);
+}
 
 __device__ __forceinline__ double bnd_eval(int form, double c0, double e0, double c1, double e1,
                                            double tau) {
@@ -212,10 +234,13 @@ struct KArgs {
   const double* mon_rebate;
   double* v_out;
   double* bnd;      // workspace: Dirichlet values [B][W][n_pad][2]
+  double* zg;       // workspace: correction tables [B][2][lz][NPT+1] (ZG variants)
   int n_pad;        // n_time rounded up to a multiple of 64
 };
 
-template <int IT, int W, int NPT>
+// ZG: the Sherman-Morrison table lives in the global workspace instead of
+// LDS -- the fallback for correction extents too long for LDS (|fm| -> 1).
+template <int IT, int W, int NPT, int ZG = 0>
 struct Geo {
   static constexpr int L = 64 * W;
   static constexpr int SPB = 1;  // one scenario per workgroup (LDS sized per scenario)
@@ -225,17 +250,17 @@ struct Geo {
 };
 
 // doubles of LDS per scenario
-template <int IT, int W, int NPT>
+template <int IT, int W, int NPT, int ZG = 0>
 __host__ __device__ inline int lds_doubles_per_scen(int lz) {
-  return 2 * lz * (NPT + 1) + (Geo<IT, W, NPT>::kPhiLds ? 64 * W * NPT : 0) +
+  return (ZG ? 0 : 2 * lz * (NPT + 1)) + (Geo<IT, W, NPT, ZG>::kPhiLds ? 64 * W * NPT : 0) +
          (W > 1 ? Xch<W>::kSize : 0);
 }
 
-template <int IT, int W, int NPT>
+template <int IT, int W, int NPT, int ZG = 0>
 __global__ void __launch_bounds__(64 * W)
 fdcn_march(KArgs A) {
-  constexpr int L = Geo<IT, W, NPT>::L;
-  constexpr int SPB = Geo<IT, W, NPT>::SPB;
+  constexpr int L = Geo<IT, W, NPT, ZG>::L;
+  constexpr int SPB = Geo<IT, W, NPT, ZG>::SPB;
   extern __shared__ __attribute__((aligned(16))) double lds[];
 
   const int lane = threadIdx.x & 63;
@@ -249,10 +274,11 @@ fdcn_march(KArgs A) {
   const int n_nodes = A.n_nodes;
   const int n_int = n_nodes - 2;
   const int lz = A.lz;
-  constexpr bool kPhiLds = Geo<IT, W, NPT>::kPhiLds;
-  double* my = lds + (size_t)scen_in_blk * lds_doubles_per_scen<IT, W, NPT>(lz);
-  double* ztab = my;                                  // SM table [2][lz][NPT+1]
-  double* phit = my + 2 * lz * (NPT + 1);             // payoff [NPT][L] (kPhiLds)
+  constexpr bool kPhiLds = Geo<IT, W, NPT, ZG>::kPhiLds;
+  double* my = lds + (size_t)scen_in_blk * lds_doubles_per_scen<IT, W, NPT, ZG>(lz);
+  // SM table [2][lz][NPT+1]: LDS, or this scenario's workspace slice (ZG)
+  double* ztab = ZG ? A.zg + (size_t)scen * 2 * lz * (NPT + 1) : my;
+  double* phit = my + (ZG ? 0 : 2 * lz * (NPT + 1));  // payoff [NPT][L] (kPhiLds)
   double* xch = phit + (kPhiLds ? L * NPT : 0);       // exchange area (W > 1)
   (void)xch;
 
@@ -904,18 +930,25 @@ struct Variant {
   KernelFn fn;
   int threads, spb;
   int (*lds_per_scen)(int lz);  // the kernel's own LDS layout, in doubles
+  int zg;                       // correction table in the workspace
 };
 
-template <int IT, int W, int NPT>
+template <int IT, int W, int NPT, int ZG = 0>
 Variant mk() {
-  return Variant{IT, W, NPT, &fdcn_march<IT, W, NPT>, Geo<IT, W, NPT>::kThreads,
-                 Geo<IT, W, NPT>::SPB, &lds_doubles_per_scen<IT, W, NPT>};
+  return Variant{IT, W, NPT, &fdcn_march<IT, W, NPT, ZG>, Geo<IT, W, NPT, ZG>::kThreads,
+                 Geo<IT, W, NPT, ZG>::SPB, &lds_doubles_per_scen<IT, W, NPT, ZG>, ZG};
 }
 
+// W=1: throughput (one wavefront per scenario).  W>1: grids beyond 64*64
+// nodes and small batches (latency).  W=16 workgroups are capped at 128
+// VGPRs (16 waves on one CU), so they use short chunks.
 #define FDCN_VARIANTS(IT)                                                                   \
   mk<IT, 1, 4>(), mk<IT, 1, 8>(), mk<IT, 1, 12>(), mk<IT, 1, 16>(), mk<IT, 1, 24>(),        \
-      mk<IT, 1, 32>(), mk<IT, 1, 40>(), mk<IT, 1, 48>(), mk<IT, 1, 64>(), mk<IT, 2, 40>(),  \
-      mk<IT, 4, 24>(), mk<IT, 4, 40>(), mk<IT, 8, 40>(), mk<IT, 16, 24>(), mk<IT, 16, 40>()
+      mk<IT, 1, 32>(), mk<IT, 1, 40>(), mk<IT, 1, 48>(), mk<IT, 1, 64>(), mk<IT, 2, 16>(),  \
+      mk<IT, 2, 32>(), mk<IT, 2, 40>(), mk<IT, 4, 8>(), mk<IT, 4, 16>(), mk<IT, 4, 24>(),   \
+      mk<IT, 4, 40>(), mk<IT, 8, 8>(), mk<IT, 8, 16>(), mk<IT, 8, 40>(), mk<IT, 16, 8>(),   \
+      mk<IT, 16, 24>(), mk<IT, 16, 40>(), mk<IT, 1, 64, 1>(), mk<IT, 4, 40, 1>(),           \
+      mk<IT, 8, 40, 1>(), mk<IT, 16, 40, 1>()
 
 const Variant kVariants[] = {FDCN_VARIANTS(0), FDCN_VARIANTS(1)};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
@@ -936,29 +969,66 @@ constexpr size_t kLdsLimit = 160 * 1024;
 
 // Choose the variant: fewest waves per scenario, then the least padding,
 // among those whose LDS (correction table + payoff) fits one CU.
-const Variant* choose(int n_nodes, int it, int k_cap) {
+bool fits(const Variant& v, int n_int, int k_cap, bool no_idle_wave = true) {
+  const int L_act = (n_int + v.npt - 1) / v.npt;
+  const int L_short = L_act * v.npt - n_int;
+  if (L_act > 64 * v.w || L_short >= L_act || v.npt > n_int) return false;
+  if (no_idle_wave && L_act <= 64 * (v.w - 1)) return false;
+  const int kc = k_cap > 0 ? k_cap : (n_int < 256 ? n_int : 256);
+  return sizeof(double) * (size_t)lds_doubles(v, lz_for(v, n_int, kc)) <= kLdsLimit;
+}
+
+// Waves the chip keeps resident at the design occupancy (256 CUs x 8).
+constexpr long kResidentWaves = 2048;
+
+// Variant choice.  Large batches (the throughput case): fewest waves per
+// scenario, then the least padding.  Batches too small to fill the chip
+// (B * W_min < kResidentWaves / 2) whose chunks are long (NPT >= 48): spread
+// each scenario over more waves, down to 16-node chunks, while the batch
+// still fits in one residency round.  FDCN_VARIANT="W,NPT" forces a variant
+// (tuning/diagnostics only).
+const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
   const int n_int = n_nodes - 2;
   if (n_int < 3) return nullptr;
+  if (const char* f = getenv("FDCN_VARIANT")) {
+    int w = 0, npt = 0;
+    if (sscanf(f, "%d,%d", &w, &npt) == 2)
+      for (int zg = 0; zg < 2; ++zg)
+        for (int i = 0; i < kNumVariants; ++i)
+          if (kVariants[i].it == it && kVariants[i].w == w && kVariants[i].npt == npt &&
+              kVariants[i].zg == zg && fits(kVariants[i], n_int, k_cap, zg == 0))
+            return &kVariants[i];
+  }
   const Variant* best = nullptr;
   long best_slots = 0;
   int best_w = 0;
-  for (int i = 0; i < kNumVariants; ++i) {
-    const Variant& v = kVariants[i];
-    if (v.it != it) continue;
-    if (best && v.w > best_w) continue;
-    const int L_act = (n_int + v.npt - 1) / v.npt;
-    const int L_short = L_act * v.npt - n_int;
-    if (L_act > 64 * v.w || L_short >= L_act || v.npt > n_int) continue;
-    const int kc = k_cap > 0 ? k_cap : (n_int < 256 ? n_int : 256);
-    if (sizeof(double) * (size_t)lds_doubles(v, lz_for(v, n_int, kc)) > kLdsLimit) continue;
-    const long slots = (long)64 * v.w * v.npt;
-    if (!best || v.w < best_w || slots < best_slots) {
-      best = &v;
-      best_slots = slots;
-      best_w = v.w;
+  // idle waves (a grid just above a variant's size) only when nothing else
+  // fits, e.g. a large correction table that needs the LDS of a wider
+  // variant; the table in the global workspace (ZG) only after that
+  for (int pass = 0; pass < 3 && !best; ++pass) {
+    for (int i = 0; i < kNumVariants; ++i) {
+      const Variant& v = kVariants[i];
+      if (v.it != it || v.zg != (pass == 2) || !fits(v, n_int, k_cap, pass == 0)) continue;
+      const long slots = (long)64 * v.w * v.npt;
+      if (!best || v.w < best_w || (v.w == best_w && slots < best_slots)) {
+        best = &v;
+        best_slots = slots;
+        best_w = v.w;
+      }
     }
   }
-  return best;
+  // Small batch of long chunks: the measured win is splitting 48-64-node
+  // chunks to ~16 across waves (config 5, one 4096-node solve: 17.1 -> 12.8
+  // ms); shorter chunks lose it again to the per-step barriers.
+  if (!best || best->npt < 48 || B * best->w >= kResidentWaves / 2) return best;
+  const Variant* lat = best;
+  for (int i = 0; i < kNumVariants; ++i) {
+    const Variant& v = kVariants[i];
+    if (v.it != it || v.zg || !fits(v, n_int, k_cap) || v.npt < 16 || B * v.w > kResidentWaves)
+      continue;
+    if (v.npt < lat->npt || (v.npt == lat->npt && v.w < lat->w)) lat = &v;
+  }
+  return lat;
 }
 
 int lds_doubles(const Variant& v, int lz) { return v.lds_per_scen(lz) * v.spb; }
@@ -969,9 +1039,14 @@ int lds_doubles(const Variant& v, int lz) { return v.lds_per_scen(lz) * v.spb; }
 
 int pad64(int n) { return ((n > 0 ? n : 1) + 63) / 64 * 64; }
 
-// workspace bytes per scenario: one (lo, hi) Dirichlet pair per step and wave
-size_t ws_bytes_per_scen(const Variant& v, int n_time) {
+// workspace bytes per scenario: one (lo, hi) Dirichlet pair per step and
+// wave; ZG variants add the correction table [2][lz][NPT+1]
+size_t bnd_bytes_per_scen(const Variant& v, int n_time) {
   return sizeof(double) * 2 * (size_t)pad64(n_time) * (size_t)v.w;
+}
+size_t ws_bytes_per_scen(const Variant& v, int n_time, int lz) {
+  return bnd_bytes_per_scen(v, n_time) +
+         (v.zg ? sizeof(double) * 2 * (size_t)lz * (size_t)(v.npt + 1) : 0);
 }
 
 double host_fm(double theta, const double* P) {
@@ -999,7 +1074,7 @@ int launch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   int rc = validate_common(B, n_nodes, n_time, n_ranna);
   if (rc) return rc;
   if (B == 0) return FDCN_OK;
-  const Variant* v = choose(n_nodes, it, k_cap);
+  const Variant* v = choose(n_nodes, it, k_cap, B);
   if (!v) return fail(FDCN_EINVAL, "unsupported n_nodes=%d", n_nodes);
   const int n_int = n_nodes - 2;
   if (k_cap <= 0) k_cap = n_int < 256 ? n_int : 256;
@@ -1022,13 +1097,14 @@ int launch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   a.mon_rebate = mon_rebate;
   a.v_out = v_out;
   a.n_pad = pad64(n_time);
-  const size_t ws_bytes = ws_bytes_per_scen(*v, n_time) * (size_t)B;
+  const size_t ws_bytes = ws_bytes_per_scen(*v, n_time, lz) * (size_t)B;
   bool own_ws = false;
   if (!workspace) {  // stream-ordered scratch, released after the launch
     HIP_TRY(hipMallocAsync((void**)&workspace, ws_bytes, stream));
     own_ws = true;
   }
   a.bnd = workspace;
+  a.zg = workspace + bnd_bytes_per_scen(*v, n_time) / sizeof(double) * (size_t)B;
   if (lds > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute((const void*)v->fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
@@ -1110,7 +1186,7 @@ int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ran
   {
     int32_t w_, npt_, spb_, lds_;
     int64_t ws_ = 0;
-    rc = fdcn_plan(n_nodes, n_time, it, k_cap, &w_, &npt_, &spb_, &lds_, &ws_);
+    rc = fdcn_plan(B, n_nodes, n_time, it, k_cap, &w_, &npt_, &spb_, &lds_, &ws_);
     if (rc == FDCN_OK && ws_ > 0 && hipMalloc((void**)&dW, (size_t)ws_ * B) != hipSuccess) {
       cleanup();
       return fail(FDCN_ENOMEM, "hipMalloc(workspace) failed");
@@ -1151,11 +1227,11 @@ int fdcn_sm_extent(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   return k;
 }
 
-int fdcn_plan(int32_t n_nodes, int32_t n_time, int32_t it_mode, int32_t k_cap, int32_t* waves,
-              int32_t* npt, int32_t* scen_per_block, int32_t* lds_bytes,
+int fdcn_plan(int32_t B, int32_t n_nodes, int32_t n_time, int32_t it_mode, int32_t k_cap,
+              int32_t* waves, int32_t* npt, int32_t* scen_per_block, int32_t* lds_bytes,
               int64_t* ws_bytes_per_scen) {
   if (n_time < 0) return fail(FDCN_EINVAL, "n_time must be >= 0 (got %d)", n_time);
-  const Variant* v = choose(n_nodes, it_mode ? 1 : 0, k_cap);
+  const Variant* v = choose(n_nodes, it_mode ? 1 : 0, k_cap, B > 0 ? B : 1);
   if (!v) return fail(FDCN_EINVAL, "unsupported n_nodes=%d", n_nodes);
   const int n_int = n_nodes - 2;
   if (k_cap <= 0) k_cap = n_int < 256 ? n_int : 256;
@@ -1166,7 +1242,7 @@ int fdcn_plan(int32_t n_nodes, int32_t n_time, int32_t it_mode, int32_t k_cap, i
   if (npt) *npt = v->npt;
   if (scen_per_block) *scen_per_block = v->spb;
   if (lds_bytes) *lds_bytes = (int32_t)lds;
-  if (ws_bytes_per_scen) *ws_bytes_per_scen = (int64_t)::ws_bytes_per_scen(*v, n_time);
+  if (ws_bytes_per_scen) *ws_bytes_per_scen = (int64_t)::ws_bytes_per_scen(*v, n_time, lz);
   return FDCN_OK;
 }
 
