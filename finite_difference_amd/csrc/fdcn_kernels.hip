@@ -139,6 +139,8 @@ struct Phase {
   double fm, bm;      // -A_L/r, -A_U/r
   double inv_r;
   double kappa;       // A_L A_U / r
+  double pl, pu;      // -A_L, -A_U (unscaled Dirichlet couplings, IT form)
+  double c2;          // (1 - theta) / theta
 };
 
 __device__ __forceinline__ Phase make_phase(double theta, double dt, double a, double c,
@@ -160,6 +162,9 @@ __device__ __forceinline__ Phase make_phase(double theta, double dt, double a, d
   p.fm = -AL * p.inv_r;
   p.bm = -AU * p.inv_r;
   p.kappa = AL * AU * p.inv_r;
+  p.pl = uni(-AL);
+  p.pu = uni(-AU);
+  p.c2 = uni((1.0 - theta) / theta);
   // wave-uniform: keep in SGPRs
   p.inv_r = uni(p.inv_r);
   p.bl = uni(p.bl);
@@ -331,9 +336,11 @@ fdcn_march(KArgs A) {
   int nst_f = 6, nst_b = 6;         // scan stages that carry weight above 1e-18
   Phase ph;
   double V[NPT];
-  double X = 0.0;  // node 0 of the shifted RHS layout (see solve)
-  double MU[NPT];  // Ikonen-Toivanen multiplier, stored scaled: mu = dt * lambda
-  (void)MU;
+  double X = 0.0;  // node 0 of the shifted RHS layout (CN; see solve)
+  // IT: the second state vector Q = V/theta - W, where W is the last
+  // pre-projection value (V = max(phi, W)); see the IT step below
+  double QS[NPT];
+  (void)QS;
 
   auto setup_scan = [&](const Phase& p) __attribute__((always_inline)) {
     if constexpr (W > 1) __syncthreads();  // previous readers of Ftot/Gtot are done
@@ -386,13 +393,16 @@ fdcn_march(KArgs A) {
   unsigned long long st_prev = 0;
   bool st_on = false;  // count only inside the time loop
 #endif
-  // Forward + backward sweeps.  Input: rhs/r in the SHIFTED layout left by
-  // the in-place RHS (node 0 in X, node k >= 1 in V[k-1]); output: the
-  // solution in the natural layout (node k in V[k]).  The forward pass works
-  // in place on the shifted slots; the last backward pass writes node k into
-  // V[k] while reading node k's forward value from V[k-1], which undoes the
-  // shift at no cost.
-  auto R = [&](int k) -> double& { return k == 0 ? X : V[k - 1]; };
+  // Forward + backward sweeps.  CN input: rhs/r in the SHIFTED layout left by
+  // the in-place RHS (node 0 in X, node k >= 1 in V[k-1]); the last backward
+  // pass writes node k into V[k] while reading node k's forward value from
+  // V[k-1], which undoes the shift at no cost.  IT input: the unscaled rhs in
+  // the natural layout (node k in V[k]); every pass works in place and the
+  // result is r times the solution.  Output: natural layout.
+  auto R = [&](int k) -> double& {
+    if constexpr (IT) return V[k];
+    else return k == 0 ? X : V[k - 1];
+  };
   auto solve = [&](const Phase& p) __attribute__((always_inline)) {
     const double fm = p.fm, bm = p.bm;
     // forward pass 1: zero-carry end value of every sub-chain
@@ -482,30 +492,47 @@ fdcn_march(KArgs A) {
     if (lane == 63) cinb = cwb;
     if (!active) cinb = 0.0;
     FDCN_STAMP(st_acc, st_prev, 6);
-    // backward pass 2 (unshifting).  Sub-chain j-1 writes V[jM-1], which
-    // holds sub-chain j's last input (node jM): read those first.
-    double wbot[S];
-#pragma unroll
-    for (int j = 1; j < S; ++j) wbot[j] = R(j * M);
     c[S - 1] = cinb;
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) c[j] = fma(j + 1 == S - 1 ? mulLB : bmM, c[j + 1], a[j + 1]);
-    // y_k = mul*y_{k+1} + w_k written over V[k] (whose value, w_{k+1}, was
-    // read one node earlier): the "+v" tie pins y_k to V[k]'s register so
-    // the vector stays in one register set.  The S sub-chains are issued
-    // round-robin (one asm statement per instruction, volatile to keep that
-    // order) so S independent FMAs are in flight.
+    if constexpr (IT) {
+      // backward pass 2 in place (natural layout): y_k = mul*y_{k+1} + w_k
+      // over V[k]; the S sub-chains round-robin, as below
 #pragma unroll
-    for (int i = M - 1; i >= 0; --i) {
+      for (int i = M - 1; i >= 0; --i) {
 #pragma unroll
-      for (int j = 0; j < S; ++j) {
-        const int k = j * M + i;
-        const double wk = (i == 0 && j > 0) ? wbot[j] : R(k);
-        const double yn = (i == M - 1) ? c[j] : V[k + 1];
-        if (k == NPT - 1)
-          asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "v"(glast), "v"(yn), "v"(wk));
-        else
-          asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "s"(bm), "v"(yn), "v"(wk));
+        for (int j = 0; j < S; ++j) {
+          const int k = j * M + i;
+          const double yn = (i == M - 1) ? c[j] : V[k + 1];
+          if (k == NPT - 1)
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(V[k]) : "v"(glast), "v"(yn));
+          else
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(V[k]) : "s"(bm), "v"(yn));
+        }
+      }
+    } else {
+      // backward pass 2 (unshifting).  Sub-chain j-1 writes V[jM-1], which
+      // holds sub-chain j's last input (node jM): read those first.
+      double wbot[S];
+#pragma unroll
+      for (int j = 1; j < S; ++j) wbot[j] = R(j * M);
+      // y_k = mul*y_{k+1} + w_k written over V[k] (whose value, w_{k+1}, was
+      // read one node earlier): the "+v" tie pins y_k to V[k]'s register so
+      // the vector stays in one register set.  The S sub-chains are issued
+      // round-robin (one asm statement per instruction, volatile to keep that
+      // order) so S independent FMAs are in flight.
+#pragma unroll
+      for (int i = M - 1; i >= 0; --i) {
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          const int k = j * M + i;
+          const double wk = (i == 0 && j > 0) ? wbot[j] : R(k);
+          const double yn = (i == M - 1) ? c[j] : V[k + 1];
+          if (k == NPT - 1)
+            asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "v"(glast), "v"(yn), "v"(wk));
+          else
+            asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "s"(bm), "v"(yn), "v"(wk));
+        }
       }
     }
   };
@@ -527,7 +554,10 @@ fdcn_march(KArgs A) {
   auto build_sm = [&](const Phase& p, int tab) __attribute__((always_inline)) -> double {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) V[k] = 0.0;
-    X = (t == 0) ? p.inv_r : 0.0;  // e0 / r in the shifted layout
+    // e0/r (CN: shifted layout, scaled input), so the table is (L U)^-1 e0 in
+    // both forms; the IT form's r-scaled solution is corrected with the same
+    // table and then scaled as a whole
+    R(0) = (t == 0) ? p.inv_r : 0.0;
     solve(p);
     if (t < lz) {
 #pragma unroll
@@ -569,11 +599,14 @@ fdcn_march(KArgs A) {
   }
   const double* pin = IT ? A.payoff + (size_t)scen * n_nodes : nullptr;
   if constexpr (IT) {
+    if (shrt) V[NPT - 1] = 0.0;  // phantom slot: exact zero (the CN rhs overwrites it)
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int node = s_t + 1 + k;
       if constexpr (kPhiLds) phit[k * L + t] = (active && node <= n_int) ? pin[node] : 0.0;
-      MU[k] = 0.0;
+      // lambda = 0 at the start (fd_american_equity.py:612): W = V, so
+      // Q = (1/theta_0 - 1) V
+      QS[k] = A.n_ranna > 0 ? 0.0 : V[k];
     }
   }
   const int ko_lo = uni_i(I[FDCN_I_KO_LO]);
@@ -622,7 +655,7 @@ fdcn_march(KArgs A) {
     }
   }
 
-  if constexpr (W > 1) {
+  if constexpr (W > 1 && !IT) {
     if (lane == 0) xch[Xch<W>::kFirst + wave] = V[0];
     if (lane == 63) xch[Xch<W>::kLast + wave] = shrt ? V[NPT - 2] : V[NPT - 1];
   }
@@ -642,7 +675,7 @@ fdcn_march(KArgs A) {
   double2 bnd_cur = make_double2(0.0, 0.0);
   double2 bnd_nxt = bnd[lane];  // steps 0..63
   double halo_l = 0.0, halo_r = 0.0;
-  if constexpr (W == 1) {
+  if constexpr (W == 1 && !IT) {
     halo_l = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
     halo_r = shfl_dn1(V[0], 1);
   }
@@ -667,7 +700,22 @@ fdcn_march(KArgs A) {
     const double hi_new = read_lane(bnd_cur.y, m & 63);
 
     FDCN_STAMP(st_acc, st_prev, 0);
-    // ---- 1. rhs/r ----------------------------------------------------------
+    // ---- 1. rhs ------------------------------------------------------------
+    if constexpr (IT) {
+      // IT form: the reference step  A x = B V + dt lambda  (+ Dirichlet
+      // terms; fd_american_equity.py:681-698) with B = (I - (1-theta) A) /
+      // theta and dt lambda = V - W (W: last pre-projection value) reads
+      //   A (x + c2 V) = V/theta + V - W = V + Q,   c2 = (1-theta)/theta,
+      // plus (-A_L)(lo_new + c2 lo_old) at node 0 and (-A_U)(hi_new + c2
+      // hi_old) at the last node.  The rhs is pointwise: no stencil and no
+      // neighbour exchange.  Unscaled, so the solve returns r (x + c2 V).
+      const double blo = ph.pl * fma(ph.c2, V0, lo_new);
+      const double bhi = ph.pu * fma(ph.c2, VN, hi_new);
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) V[k] += QS[k];
+      if (t == 0) V[0] += blo;
+      if (t == L_act - 1) V[NPT - 1] += bhi;  // the last active lane is never short
+    } else {
     if constexpr (W > 1) __syncthreads();  // halos of the previous step
     // neighbours' edge values: shuffled at the end of the previous step (W=1)
     // so their latency overlaps the tail of that step
@@ -698,8 +746,7 @@ fdcn_march(KArgs A) {
       //   op1: acc_j  = B_L * V_{j-1}     (acc_0 = X, acc_j = V[j-1])
       //   op2: acc_j += B_C * V_j
       //   op3: acc_j += B_U * V_{j+1}     (V_NPT = right)
-      //   op4: acc_j += mu_j / r          (IT)
-      constexpr int kOps = IT ? 4 : 3;
+      constexpr int kOps = 3;
 #pragma unroll
       for (int st = 0; st < NPT + kOps - 1; ++st) {
 #pragma unroll
@@ -714,19 +761,15 @@ fdcn_march(KArgs A) {
               asm volatile("v_mul_f64 %0, %1, %2" : "=v"(X) : "s"(ph.bc), "v"(V[0]));
             else if (op == 2)
               asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(X) : "s"(ph.bu), "v"(V[1]));
-            else if (op == 4)
-              asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(X) : "s"(ph.inv_r), "v"(MU[0]));
             continue;
           }
           if (op == 1) {
             asm volatile("v_mul_f64 %0, %1, %0" : "+v"(acc) : "s"(ph.bl));
           } else if (op == 2) {
             asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(acc) : "s"(ph.bc), "v"(V[j]));
-          } else if (op == 3) {
+          } else {
             const double nxt = (j < NPT - 1) ? V[j + 1] : right;
             asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(acc) : "s"(ph.bu), "v"(nxt));
-          } else {
-            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(acc) : "s"(ph.inv_r), "v"(MU[j]));
           }
         }
       }
@@ -735,6 +778,7 @@ fdcn_march(KArgs A) {
     if (t == 0) X = fma(ph.fm, lo_new, X);                                  // node 0
     if (t == L_act - 1) V[NPT - 2] = fma(ph.bm, hi_new, V[NPT - 2]);        // node NPT-1
     if (shrt) V[NPT - 2] = 0.0;  // the phantom node's rhs
+    }  // CN rhs
 
     FDCN_STAMP(st_acc, st_prev, 1);
     // ---- 2. tridiagonal solve ---------------------------------------------
@@ -762,6 +806,8 @@ fdcn_march(KArgs A) {
     }
     FDCN_STAMP(st_acc, st_prev, 8);
     // ---- 3. early exercise / boundaries / knock-out ------------------------
+    const double cq = (m + 1 < A.n_ranna) ? 1.0 : 2.0;  // 1/theta of the next step (IT)
+    (void)cq;
     {
       const int poff = opaque(kPhiLds ? t : s_t + 1);
       auto phi_at = [&](int k) -> double {
@@ -794,42 +840,46 @@ fdcn_march(KArgs A) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) V[k + i] = fma(g, zk[i], V[k + i]);
         } else {
-          // x = y + g z, then fd_american_equity.py:704-717 with mu = dt*lambda:
-          //   v~ = x - mu;  mu' = max(phi - v~, 0);  V' = max(phi, v~)
-          // (= dt * max(lambda + (phi - x)/dt, 0) and max(phi, x - dt lambda)
-          // in exact arithmetic; the reference's compare-select can differ
-          // only in the sign of an exact zero).  In place, the four nodes'
-          // dependent chains interleaved.
+          // r x~ = y~ + g z (Sherman-Morrison on the r-scaled solution,
+          // x~ = x + c2 V), then the Ikonen-Toivanen update
+          // (fd_american_equity.py:704-717):
+          //   W  = x - dt lambda = x~ - Q
+          //   V' = max(phi, W)
+          //   Q' = V'/theta' - W               (theta' of the next step: cq)
+          // with dt lambda' = V' - W = max(phi - W, 0), the reference's
+          // multiplier update max(lambda + (phi - x)/dt, 0) in exact
+          // arithmetic.  In place (W lives in Q's registers), the four
+          // nodes' dependent chains interleaved.
           asm volatile(
               "v_fma_f64 %0, %12, %13, %0\n\t"
               "v_fma_f64 %1, %12, %14, %1\n\t"
               "v_fma_f64 %2, %12, %15, %2\n\t"
               "v_fma_f64 %3, %12, %16, %3\n\t"
-              "v_add_f64 %0, %0, -%4\n\t"
-              "v_add_f64 %1, %1, -%5\n\t"
-              "v_add_f64 %2, %2, -%6\n\t"
-              "v_add_f64 %3, %3, -%7\n\t"
-              "v_add_f64 %4, %8, -%0\n\t"
-              "v_add_f64 %5, %9, -%1\n\t"
-              "v_add_f64 %6, %10, -%2\n\t"
-              "v_add_f64 %7, %11, -%3\n\t"
-              "v_max_f64 %0, %8, %0\n\t"
-              "v_max_f64 %1, %9, %1\n\t"
-              "v_max_f64 %2, %10, %2\n\t"
-              "v_max_f64 %3, %11, %3\n\t"
-              "v_max_f64 %4, %4, 0\n\t"
-              "v_max_f64 %5, %5, 0\n\t"
-              "v_max_f64 %6, %6, 0\n\t"
-              "v_max_f64 %7, %7, 0"
-              : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(MU[k]),
-                "+v"(MU[k + 1]), "+v"(MU[k + 2]), "+v"(MU[k + 3])
+              "v_fma_f64 %4, %17, %0, -%4\n\t"
+              "v_fma_f64 %5, %17, %1, -%5\n\t"
+              "v_fma_f64 %6, %17, %2, -%6\n\t"
+              "v_fma_f64 %7, %17, %3, -%7\n\t"
+              "v_max_f64 %0, %8, %4\n\t"
+              "v_max_f64 %1, %9, %5\n\t"
+              "v_max_f64 %2, %10, %6\n\t"
+              "v_max_f64 %3, %11, %7\n\t"
+              "v_fma_f64 %4, %18, %0, -%4\n\t"
+              "v_fma_f64 %5, %18, %1, -%5\n\t"
+              "v_fma_f64 %6, %18, %2, -%6\n\t"
+              "v_fma_f64 %7, %18, %3, -%7"
+              : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(QS[k]),
+                "+v"(QS[k + 1]), "+v"(QS[k + 2]), "+v"(QS[k + 3])
               : "v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]), "v"(g), "v"(zk[0]),
-                "v"(zk[1]), "v"(zk[2]), "v"(zk[3]));
+                "v"(zk[1]), "v"(zk[2]), "v"(zk[3]), "s"(ph.inv_r), "s"(cq));
         }
       }
     }
     if constexpr (IT) {
-      if (shrt) MU[NPT - 1] = 0.0;
+      // the phantom slot of a short lane stays an exact zero (zero rhs)
+      if (shrt) {
+        V[NPT - 1] = 0.0;
+        QS[NPT - 1] = 0.0;
+      }
     }
     V0 = lo_new;
     VN = hi_new;
@@ -869,7 +919,9 @@ fdcn_march(KArgs A) {
         pf_reb = (mpos + 1 < mend) ? uni(A.mon_rebate[mpos + 1]) : 0.0;
       }
     }
-    if constexpr (W > 1) {
+    if constexpr (IT) {
+      // pointwise rhs: no halos
+    } else if constexpr (W > 1) {
       if (lane == 0) xch[Xch<W>::kFirst + wave] = V[0];
       if (lane == 63) xch[Xch<W>::kLast + wave] = shrt ? V[NPT - 2] : V[NPT - 1];
     } else {
