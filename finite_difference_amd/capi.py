@@ -15,7 +15,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(HERE, "_lib")
-LIB_PATH = os.path.join(LIB_DIR, "libfdcn.so")
+# FDCN_LIB points at an alternative build of the same library (A/B timing of
+# kernel variants only; unset in every test, smoke and bench run)
+LIB_PATH = os.environ.get("FDCN_LIB") or os.path.join(LIB_DIR, "libfdcn.so")
 REPO_ROOT = os.path.dirname(HERE)
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "fdcn.h")
 

@@ -139,8 +139,10 @@ struct Phase {
   double fm, bm;      // -A_L/r, -A_U/r
   double inv_r;
   double kappa;       // A_L A_U / r
-  double pl, pu;      // -A_L, -A_U (unscaled Dirichlet couplings, IT form)
+  double pl, pu;      // -A_L, -A_U (unscaled Dirichlet couplings, theta form)
   double c2;          // (1 - theta) / theta
+  double s;           // 1 / (theta r)
+  double th;          // theta
 };
 
 __device__ __forceinline__ Phase make_phase(double theta, double dt, double a, double c,
@@ -165,6 +167,8 @@ __device__ __forceinline__ Phase make_phase(double theta, double dt, double a, d
   p.pl = uni(-AL);
   p.pu = uni(-AU);
   p.c2 = uni((1.0 - theta) / theta);
+  p.s = uni(p.inv_r / theta);
+  p.th = uni(theta);
   // wave-uniform: keep in SGPRs
   p.inv_r = uni(p.inv_r);
   p.bl = uni(p.bl);
@@ -335,12 +339,28 @@ fdcn_march(KArgs A) {
   double fmM = 0.0, bmM = 0.0;      // products across a full sub-chain
   int nst_f = 6, nst_b = 6;         // scan stages that carry weight above 1e-18
   Phase ph;
+  // Step forms (see the time loop):
+  //   IT            state (V, Q), pointwise rhs V + Q, solve in place on V
+  //   CN, kSplit    state V, rhs V (+ boundary terms), solve into T
+  //   CN, stencil   state V, 3-point rhs in place (shifted layout); the
+  //                 variants whose V + T would not fit the register budget
+#ifdef FDCN_NO_SPLIT  // A/B builds only (tools/ab_build.sh)
+  constexpr bool kSplit = false;
+#else
+  constexpr bool kSplit = !IT && (W == 16 ? NPT <= 16 : NPT <= 40);
+#endif
+  constexpr bool kNatural = IT || kSplit;  // solve input in the natural layout
   double V[NPT];
-  double X = 0.0;  // node 0 of the shifted RHS layout (CN; see solve)
+  double X = 0.0;  // node 0 of the shifted RHS layout (stencil CN; see solve)
   // IT: the second state vector Q = V/theta - W, where W is the last
   // pre-projection value (V = max(phi, W)); see the IT step below
-  double QS[NPT];
+  double QS[IT ? NPT : 1];
+  double T[kSplit ? NPT : 1];  // kSplit: the solve's work vector
+  double vb0 = 0.0, vb1 = 0.0;  // kSplit: rhs of the chunk's first/last node
   (void)QS;
+  (void)T;
+  (void)vb0;
+  (void)vb1;
 
   auto setup_scan = [&](const Phase& p) __attribute__((always_inline)) {
     if constexpr (W > 1) __syncthreads();  // previous readers of Ftot/Gtot are done
@@ -393,15 +413,27 @@ fdcn_march(KArgs A) {
   unsigned long long st_prev = 0;
   bool st_on = false;  // count only inside the time loop
 #endif
-  // Forward + backward sweeps.  CN input: rhs/r in the SHIFTED layout left by
-  // the in-place RHS (node 0 in X, node k >= 1 in V[k-1]); the last backward
-  // pass writes node k into V[k] while reading node k's forward value from
-  // V[k-1], which undoes the shift at no cost.  IT input: the unscaled rhs in
-  // the natural layout (node k in V[k]); every pass works in place and the
-  // result is r times the solution.  Output: natural layout.
-  auto R = [&](int k) -> double& {
+  // Forward + backward sweeps.  Stencil CN input: rhs/r in the SHIFTED
+  // layout left by the in-place RHS (node 0 in X, node k >= 1 in V[k-1]);
+  // the last backward pass writes node k into V[k] while reading node k's
+  // forward value from V[k-1], which undoes the shift at no cost; output in
+  // V.  IT / kSplit input: the unscaled rhs in the natural layout (In); the
+  // passes work in place on Wr (V for IT, T for kSplit) and return r times
+  // the solution there.
+  auto In = [&](int k) -> double {
     if constexpr (IT) return V[k];
+    else if constexpr (kSplit) return k == 0 ? vb0 : (k == NPT - 1 ? vb1 : V[k]);
     else return k == 0 ? X : V[k - 1];
+  };
+  auto Wr = [&](int k) -> double& {
+    if constexpr (IT) return V[k];
+    else if constexpr (kSplit) return T[k];
+    else return k == 0 ? X : V[k - 1];
+  };
+  // where the solve leaves the solution (natural layout)
+  auto Out = [&](int k) -> double& {
+    if constexpr (kSplit) return T[k];
+    else return V[k];
   };
   auto solve = [&](const Phase& p) __attribute__((always_inline)) {
     const double fm = p.fm, bm = p.bm;
@@ -413,7 +445,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const int k = j * M + i;
-        w = fma(k == NPT - 1 ? mlast : fm, w, R(k));
+        w = fma(k == NPT - 1 ? mlast : fm, w, In(k));
       }
       a[j] = w;
     }
@@ -451,8 +483,8 @@ fdcn_march(KArgs A) {
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const int k = j * M + i;
-        w = fma(k == NPT - 1 ? mlast : fm, w, R(k));
-        R(k) = (k == NPT - 1 && shrt) ? 0.0 : w;
+        w = fma(k == NPT - 1 ? mlast : fm, w, In(k));
+        Wr(k) = (k == NPT - 1 && shrt) ? 0.0 : w;
       }
     }
     FDCN_STAMP(st_acc, st_prev, 4);
@@ -463,7 +495,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
       for (int i = M - 1; i >= 0; --i) {
         const int k = j * M + i;
-        y = fma(k == NPT - 1 ? glast : bm, y, R(k));
+        y = fma(k == NPT - 1 ? glast : bm, y, Wr(k));
       }
       a[j] = y;
     }
@@ -495,19 +527,19 @@ fdcn_march(KArgs A) {
     c[S - 1] = cinb;
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) c[j] = fma(j + 1 == S - 1 ? mulLB : bmM, c[j + 1], a[j + 1]);
-    if constexpr (IT) {
+    if constexpr (kNatural) {
       // backward pass 2 in place (natural layout): y_k = mul*y_{k+1} + w_k
-      // over V[k]; the S sub-chains round-robin, as below
+      // over Wr(k); the S sub-chains round-robin, as below
 #pragma unroll
       for (int i = M - 1; i >= 0; --i) {
 #pragma unroll
         for (int j = 0; j < S; ++j) {
           const int k = j * M + i;
-          const double yn = (i == M - 1) ? c[j] : V[k + 1];
+          const double yn = (i == M - 1) ? c[j] : Wr(k + 1);
           if (k == NPT - 1)
-            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(V[k]) : "v"(glast), "v"(yn));
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(Wr(k)) : "v"(glast), "v"(yn));
           else
-            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(V[k]) : "s"(bm), "v"(yn));
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(Wr(k)) : "s"(bm), "v"(yn));
         }
       }
     } else {
@@ -515,7 +547,7 @@ fdcn_march(KArgs A) {
       // holds sub-chain j's last input (node jM): read those first.
       double wbot[S];
 #pragma unroll
-      for (int j = 1; j < S; ++j) wbot[j] = R(j * M);
+      for (int j = 1; j < S; ++j) wbot[j] = Wr(j * M);
       // y_k = mul*y_{k+1} + w_k written over V[k] (whose value, w_{k+1}, was
       // read one node earlier): the "+v" tie pins y_k to V[k]'s register so
       // the vector stays in one register set.  The S sub-chains are issued
@@ -526,7 +558,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
         for (int j = 0; j < S; ++j) {
           const int k = j * M + i;
-          const double wk = (i == 0 && j > 0) ? wbot[j] : R(k);
+          const double wk = (i == 0 && j > 0) ? wbot[j] : Wr(k);
           const double yn = (i == M - 1) ? c[j] : V[k + 1];
           if (k == NPT - 1)
             asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "v"(glast), "v"(yn), "v"(wk));
@@ -554,16 +586,21 @@ fdcn_march(KArgs A) {
   auto build_sm = [&](const Phase& p, int tab) __attribute__((always_inline)) -> double {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) V[k] = 0.0;
-    // e0/r (CN: shifted layout, scaled input), so the table is (L U)^-1 e0 in
-    // both forms; the IT form's r-scaled solution is corrected with the same
-    // table and then scaled as a whole
-    R(0) = (t == 0) ? p.inv_r : 0.0;
+    // input e0/r, so the table is (L U)^-1 e0 in every form; the IT / kSplit
+    // forms correct their r-scaled solution with the same table before
+    // scaling it as a whole
+    if constexpr (kSplit) {
+      vb0 = (t == 0) ? p.inv_r : 0.0;
+      vb1 = 0.0;
+    } else {
+      Wr(0) = (t == 0) ? p.inv_r : 0.0;
+    }
     solve(p);
     if (t < lz) {
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) ztab[(tab * lz + t) * (NPT + 1) + k] = V[k];
+      for (int k = 0; k < NPT; ++k) ztab[(tab * lz + t) * (NPT + 1) + k] = Out(k);
     }
-    const double z0 = bcast_first(V[0]);
+    const double z0 = bcast_first(Out(0));
     return uni(p.kappa / (1.0 + p.kappa * z0));
   };
 
@@ -598,8 +635,10 @@ fdcn_march(KArgs A) {
     V[k] = (active && node <= n_int) ? vin[node] : 0.0;
   }
   const double* pin = IT ? A.payoff + (size_t)scen * n_nodes : nullptr;
+  if constexpr (kNatural) {
+    if (shrt) V[NPT - 1] = 0.0;  // phantom slot: exact zero (the stencil rhs overwrites it)
+  }
   if constexpr (IT) {
-    if (shrt) V[NPT - 1] = 0.0;  // phantom slot: exact zero (the CN rhs overwrites it)
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int node = s_t + 1 + k;
@@ -655,7 +694,7 @@ fdcn_march(KArgs A) {
     }
   }
 
-  if constexpr (W > 1 && !IT) {
+  if constexpr (W > 1 && !kNatural) {
     if (lane == 0) xch[Xch<W>::kFirst + wave] = V[0];
     if (lane == 63) xch[Xch<W>::kLast + wave] = shrt ? V[NPT - 2] : V[NPT - 1];
   }
@@ -675,7 +714,7 @@ fdcn_march(KArgs A) {
   double2 bnd_cur = make_double2(0.0, 0.0);
   double2 bnd_nxt = bnd[lane];  // steps 0..63
   double halo_l = 0.0, halo_r = 0.0;
-  if constexpr (W == 1 && !IT) {
+  if constexpr (W == 1 && !kNatural) {
     halo_l = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
     halo_r = shfl_dn1(V[0], 1);
   }
@@ -715,6 +754,17 @@ fdcn_march(KArgs A) {
       for (int k = 0; k < NPT; ++k) V[k] += QS[k];
       if (t == 0) V[0] += blo;
       if (t == L_act - 1) V[NPT - 1] += bhi;  // the last active lane is never short
+    } else if constexpr (kSplit) {
+      // theta form of the reference step A x = B V (+ Dirichlet terms,
+      // discrete_barrier_fdm_pricer.py:531-537) with B = (I - (1-theta) A) /
+      // theta:  A (theta x + (1-theta) V) = V + theta (-A_L)(lo_new + c2
+      // lo_old) e_0 + theta (-A_U)(hi_new + c2 hi_old) e_n.  The rhs is V
+      // itself except at the two end nodes (vb0 / vb1); the solve reads V and
+      // writes T, and x = (r u)/(theta r) - c2 V afterwards.
+      const double blo = ph.th * (ph.pl * fma(ph.c2, V0, lo_new));
+      const double bhi = ph.th * (ph.pu * fma(ph.c2, VN, hi_new));
+      vb0 = (t == 0) ? V[0] + blo : V[0];
+      vb1 = (t == L_act - 1) ? V[NPT - 1] + bhi : (shrt ? 0.0 : V[NPT - 1]);
     } else {
     if constexpr (W > 1) __syncthreads();  // halos of the previous step
     // neighbours' edge values: shuffled at the end of the previous step (W=1)
@@ -796,13 +846,21 @@ fdcn_march(KArgs A) {
     if (do_sm) {
       double y0;
       if constexpr (W == 1) {
-        y0 = read_lane(V[0], 0);
+        y0 = read_lane(Out(0), 0);
       } else {
-        y0 = (lz > 64) ? bcast_first(V[0]) : read_lane(V[0], 0);
+        y0 = (lz > 64) ? bcast_first(Out(0)) : read_lane(Out(0), 0);
       }
       g = (t < lz) ? -(smc * y0) : 0.0;
       // lane-major rows, stride NPT+1: bank-spread, immediate offsets
       zoff = opaque((tab * lz + (t < lz ? t : lz - 1)) * (NPT + 1));
+    }
+    if constexpr (kSplit) {
+      // x = s (T + g z) - c2 V: c2 = 1 for theta = 1/2; the Rannacher steps
+      // (c2 = 0) drop V instead of taking another multiply per node
+      if (m < A.n_ranna) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) V[k] = 0.0;
+      }
     }
     FDCN_STAMP(st_acc, st_prev, 8);
     // ---- 3. early exercise / boundaries / knock-out ------------------------
@@ -836,7 +894,20 @@ fdcn_march(KArgs A) {
             if constexpr (IT) pn[i] = phi_at(k + 4 + i);
           }
         }
-        if constexpr (!IT) {
+        if constexpr (kSplit) {
+          asm volatile(
+              "v_fma_f64 %4, %8, %9, %4\n\t"
+              "v_fma_f64 %5, %8, %10, %5\n\t"
+              "v_fma_f64 %6, %8, %11, %6\n\t"
+              "v_fma_f64 %7, %8, %12, %7\n\t"
+              "v_fma_f64 %0, %13, %4, -%0\n\t"
+              "v_fma_f64 %1, %13, %5, -%1\n\t"
+              "v_fma_f64 %2, %13, %6, -%2\n\t"
+              "v_fma_f64 %3, %13, %7, -%3"
+              : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(T[k]),
+                "+v"(T[k + 1]), "+v"(T[k + 2]), "+v"(T[k + 3])
+              : "v"(g), "v"(zk[0]), "v"(zk[1]), "v"(zk[2]), "v"(zk[3]), "s"(ph.s));
+        } else if constexpr (!IT) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) V[k + i] = fma(g, zk[i], V[k + i]);
         } else {
@@ -880,6 +951,8 @@ fdcn_march(KArgs A) {
         V[NPT - 1] = 0.0;
         QS[NPT - 1] = 0.0;
       }
+    } else if constexpr (kSplit) {
+      if (shrt) V[NPT - 1] = 0.0;
     }
     V0 = lo_new;
     VN = hi_new;
@@ -919,7 +992,7 @@ fdcn_march(KArgs A) {
         pf_reb = (mpos + 1 < mend) ? uni(A.mon_rebate[mpos + 1]) : 0.0;
       }
     }
-    if constexpr (IT) {
+    if constexpr (kNatural) {
       // pointwise rhs: no halos
     } else if constexpr (W > 1) {
       if (lane == 0) xch[Xch<W>::kFirst + wave] = V[0];
