@@ -229,6 +229,11 @@ class AmericanFDMPricer:
         lo, hi = self._boundaries()
         return lo.value(tau), hi.value(tau)
 
+    def _operator_rates(self) -> Tuple[float, float]:
+        """(b, q) of the log-S operator: carry, and q = 0 (discrete dividends
+        are jumps, fd_american_equity.py:242-249)."""
+        return self.carry_rate_nacc, 0.0
+
     def _boundaries(self) -> Tuple[Boundary, Boundary]:
         """Dirichlet values of fd_american_equity.py:430-448 as kernel forms."""
         r, b = self.discount_rate_nacc, self.carry_rate_nacc
@@ -307,8 +312,8 @@ class AmericanFDMPricer:
                        n_steps: int, restart_rannacher: bool) -> Solve:
         """The work of one _solve_segment call as a kernel scenario."""
         dt = (tau_end - tau_start) / float(n_steps)
-        coeffs = operator_coefficients(self.sigma, self.carry_rate_nacc, 0.0,
-                                       self.discount_rate_nacc, self._dx)
+        b, q = self._operator_rates()
+        coeffs = operator_coefficients(self.sigma, b, q, self.discount_rate_nacc, self._dx)
         lower, upper = self._boundaries()
         pay = self._payoff_array()
         return Solve(it=True, n_time=int(n_steps),

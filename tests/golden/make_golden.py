@@ -351,6 +351,42 @@ def gen_american(with_config2: bool):
     dump("american_cases.json", out)
 
 
+def gen_black76():
+    """fd_american_black76.py (AmericanFwdFDMPricer): same march, Black-76
+    coefficients (mu_x = -sigma^2/2) and discounted boundaries."""
+    _install_workalendar_stub()
+    sys.path.insert(0, REF)
+    import fd_american_black76 as m  # type: ignore
+    specs = [
+        dict(name="fwd_put_200", spot=176.39, strike=170.0, sigma=0.296783211249,
+             option_type="put", naca=math.exp(0.07053828272) - 1.0, N=200, M=200),
+        dict(name="fwd_call_160", spot=176.39, strike=170.0, sigma=0.296783211249,
+             option_type="call", naca=math.exp(0.07053828272) - 1.0, N=160, M=120),
+        dict(name="fwd_put_itm", spot=95.0, strike=110.0, sigma=0.4, option_type="put",
+             naca=0.09, N=128, M=100),
+    ]
+    cases = []
+    for s in specs:
+        c = curve(s["naca"])
+        p = m.AmericanFwdFDMPricer(spot=s["spot"], strike=s["strike"], valuation_date=VAL,
+                                   maturity_date=MAT, sigma=s["sigma"],
+                                   option_type=s["option_type"], discount_curve=c,
+                                   forward_curve=c, num_space_nodes=s["N"],
+                                   num_time_steps=s["M"], rannacher_steps=2)
+        rec = dict(name=s["name"], inputs=s)
+        rec["price_log"] = p.price_log()
+        rec["V"] = p._solve_grid()
+        rec["s_nodes"] = p.s_nodes
+        rec["price_log2"] = p.price_log2()
+        rec["greeks_log2"] = p.greeks_log2()
+        rec["attrs"] = dict(time_to_expiry=p.time_to_expiry,
+                            discount_rate_nacc=p.discount_rate_nacc, S_min=p._S_min,
+                            S_max=p._S_max, spot_snapped=p.spot_snapped,
+                            strike_snapped=p.strike_snapped, dx=p._dx)
+        cases.append(rec)
+    dump("black76_cases.json", dict(cases=cases))
+
+
 # --------------------------------------------------------------------------
 # 4. analytic engines
 # --------------------------------------------------------------------------
@@ -394,7 +430,9 @@ def gen_analytic():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["cn", "barrier", "american", "analytic"]
+    which = sys.argv[1:] or ["cn", "barrier", "american", "analytic", "black76"]
+    if "black76" in which:
+        gen_black76()
     if "cn" in which:
         gen_cn_log()
     if "barrier" in which:

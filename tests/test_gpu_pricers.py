@@ -47,6 +47,18 @@ def test_american_golden_on_gpu():
         check_greeks(p.greeks_log2(), case["greeks_log2"], "american " + case["name"])
 
 
+def test_black76_golden_on_gpu():
+    import test_black76_host as T
+    for case in T.CASES:
+        p = T.make(case, Engine())
+        V = p._solve_grid()
+        ref = np.array(case["V"])
+        assert np.max(np.abs(np.array(V) - ref)) <= 1e-10 * max(1.0, np.max(np.abs(ref)))
+        assert close("price", p.price_log(), case["price_log"])
+        assert close("price", p.price_log2(), case["price_log2"])
+        check_greeks(p.greeks_log2(), case["greeks_log2"], "black76 " + case["name"])
+
+
 def test_american_config2_full_grid():
     rec = load_golden("american_cases.json")["config2"]
     from finite_difference_amd.american import AmericanFDMPricer
