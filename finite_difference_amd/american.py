@@ -25,7 +25,7 @@ from typing import Dict, List, Literal, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import market
+from . import capi, market
 from .engine import FORM_SUM, Boundary, Engine, Solve, default_engine, operator_coefficients
 
 OptionType = Literal["call", "put"]
@@ -181,14 +181,23 @@ class AmericanFDMPricer:
         x_max = math.log(self._S_max)
         n = self.num_space_nodes
         dx = (x_max - x_min) / float(n)
-        self.x_nodes = [x_min + i * dx for i in range(n + 1)]
-        self.s_nodes = list(map(math.exp, self.x_nodes))
+        # [x_min + i * dx ...] and math.exp of each (…equity.py:372-373), in libfdcn
+        x, s = capi.log_grid(x_min, dx, n)
+        self.x_nodes = x.tolist()
+        self.s_nodes = s.tolist()
         self._dx = dx
         self._snap_critical_levels_to_grid()
         return dx
 
+    def _s_array(self) -> np.ndarray:
+        """self.s_nodes as float64 array, converted once per grid list."""
+        if getattr(self, "_s_arr_src", None) is not self.s_nodes:
+            self._s_arr = np.asarray(self.s_nodes, dtype=np.float64)
+            self._s_arr_src = self.s_nodes
+        return self._s_arr
+
     def _snap_critical_levels_to_grid(self) -> None:
-        s = np.asarray(self.s_nodes)
+        s = self._s_array()
         if s.size == 0:
             return
         if self.snap_spot_to_grid:
@@ -217,7 +226,7 @@ class AmericanFDMPricer:
     def _payoff_array(self) -> np.ndarray:
         """Vectorised _intrinsic_payoff over the grid; np.where(0.0 > e, 0.0, e)
         is exactly Python's max(e, 0.0)."""
-        s = np.asarray(self.s_nodes, dtype=np.float64)
+        s = self._s_array()
         k = self._strike_for_pde()
         e = s - k if self.option_type == "call" else k - s
         return np.where(0.0 > e, 0.0, e)

@@ -28,7 +28,7 @@ from typing import Any, Dict, List, Literal, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import market
+from . import capi, market
 from .engine import (FORM_PROD, FORM_SUM, Boundary, Engine, Solve, default_engine,
                      operator_coefficients)
 
@@ -191,8 +191,7 @@ class DiscreteBarrierFDMPricer:
         self.grid_type = grid_type
         self.sinh_alpha = sinh_alpha
         self.time_spacing = self.time_to_expiry / self.num_time_steps
-        self.time_grid = [i * self.time_to_expiry / self.num_time_steps
-                          for i in range(self.num_time_steps + 1)]
+        self._time_grid: Optional[List[float]] = None
         self.monitor_times = self._build_monitor_times_exact()
 
         self.s_nodes: List[float] = []
@@ -207,6 +206,15 @@ class DiscreteBarrierFDMPricer:
         self.grid_mode = grid_mode
         self._requested_space_nodes = int(num_space_nodes)
         self._pde_cache: Dict[tuple, Dict[str, float]] = {}
+
+    @property
+    def time_grid(self) -> List[float]:
+        """t_i = i T / N_t (:170); built on first use, since the march never
+        reads it (a 10 000-trade batch would otherwise build 10 000 lists)."""
+        if self._time_grid is None:
+            self._time_grid = [i * self.time_to_expiry / self.num_time_steps
+                               for i in range(self.num_time_steps + 1)]
+        return self._time_grid
 
     # ------------------------------------------------------------- calendar
     def _infer_denominator(self, day_count: str) -> int:
@@ -311,7 +319,8 @@ class DiscreteBarrierFDMPricer:
         x_min, x_max = math.log(self._S_min), math.log(self._S_max)
         n = self.num_space_nodes
         dx = (x_max - x_min) / n
-        s = list(map(math.exp, [x_min + i * dx for i in range(n + 1)]))
+        # [math.exp(x_min + i * dx) for i in range(n + 1)] (:358), in libfdcn
+        s = capi.log_grid(x_min, dx, n)[1].tolist()
         return _Grid(n, self.num_time_steps, self._S_min, self._S_max, dx, s)
 
     def _build_log_grid(self) -> float:

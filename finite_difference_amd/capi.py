@@ -31,8 +31,8 @@ NIPARAM = 7
 ABI_VERSION = 3
 
 EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batch_dev",
-            "fdcn_plan", "fdcn_sm_extent", "fdcn_last_error", "fdcn_device_count",
-            "fdcn_abi_version")
+            "fdcn_plan", "fdcn_sm_extent", "fdcn_log_grid", "fdcn_last_error",
+            "fdcn_device_count", "fdcn_abi_version")
 
 
 class FdcnError(RuntimeError):
@@ -72,6 +72,8 @@ def lib() -> ctypes.CDLL:
                                     ctypes.POINTER(ctypes.c_int64)]
             L.fdcn_sm_extent.restype = _I
             L.fdcn_sm_extent.argtypes = [_I, _I, _I, _I, _PD]
+            L.fdcn_log_grid.restype = _I
+            L.fdcn_log_grid.argtypes = [ctypes.c_double, ctypes.c_double, _I, _V, _V]
             L.fdcn_last_error.restype = ctypes.c_char_p
             L.fdcn_last_error.argtypes = []
             L.fdcn_device_count.restype = ctypes.c_int
@@ -171,3 +173,13 @@ def it_batch_dev(B: int, n_nodes: int, n_time: int, n_ranna: int, params_ptr: in
     _check(lib().fdcn_it_batch_dev(B, n_nodes, n_time, n_ranna, params_ptr, iparams_ptr,
                                    v_init_ptr, payoff_ptr, v_out_ptr, k_cap, workspace_ptr,
                                    stream_ptr))
+
+
+def log_grid(x_min: float, dx: float, n: int):
+    """(x, s) with x[i] = x_min + i*dx and s = exp(x) for i = 0..n, computed in
+    libfdcn with the C library's exp -- bit-identical to the reference's
+    ``[math.exp(x_min + i * dx) for i in range(n + 1)]`` (host only, no device)."""
+    x = np.empty(n + 1, dtype=np.float64)
+    s = np.empty(n + 1, dtype=np.float64)
+    _check(lib().fdcn_log_grid(float(x_min), float(dx), int(n), x.ctypes.data, s.ctypes.data))
+    return x, s

@@ -25,6 +25,8 @@ from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
+from . import capi
+
 from .engine import FORM_SUM, Boundary, Engine, Solve, default_engine, operator_coefficients
 
 SQRT_2PI = math.sqrt(2.0 * math.pi)
@@ -100,7 +102,7 @@ class DiscreteBarrierCrankNicolsonLog:
         x_min, x_max = math.log(self._S_min), math.log(self._S_max)
         N = self.N_space
         dx = (x_max - x_min) / N
-        self.s_nodes = list(map(math.exp, [x_min + i * dx for i in range(N + 1)]))
+        self.s_nodes = capi.log_grid(x_min, dx, N)[1].tolist()  # math.exp(x_min + i dx)
         return dx
 
     def _terminal_payoff(self) -> List[float]:

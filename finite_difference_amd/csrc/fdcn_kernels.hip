@@ -1406,6 +1406,17 @@ int fdcn_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                     nullptr, nullptr, v_out);
 }
 
+int fdcn_log_grid(double x_min, double dx, int32_t n, double* x, double* s) {
+#pragma clang fp contract(off)
+  if (n < 0 || !s) return fail(FDCN_EINVAL, "fdcn_log_grid: n must be >= 0 and s non-NULL");
+  for (int32_t i = 0; i <= n; ++i) {
+    const double xi = x_min + (double)i * dx;  // the reference's x_min + i * dx
+    if (x) x[i] = xi;
+    s[i] = ::exp(xi);                           // libm exp, as math.exp
+  }
+  return FDCN_OK;
+}
+
 const char* fdcn_last_error(void) { return g_err.c_str(); }
 
 int fdcn_device_count(void) {

@@ -29,6 +29,8 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
+from . import capi
+
 from .analytic import BarrierEngine, DoubleBarrier, _norm_rebate_timing, black_scholes
 from .barrier import tail_quantile
 from .engine import FORM_SUM, Boundary, Engine, Solve, default_engine, operator_coefficients
@@ -45,7 +47,7 @@ def _domain(cands: Sequence[float], sigma: float, T: float):
 def _grid(S_min: float, S_max: float, n_space: int):
     x0, x1 = math.log(S_min), math.log(S_max)
     dx = (x1 - x0) / n_space
-    return dx, list(map(math.exp, [x0 + i * dx for i in range(n_space + 1)]))
+    return dx, capi.log_grid(x0, dx, n_space)[1].tolist()  # math.exp(x0 + i dx)
 
 
 def _steps(n_time: int, T: float, monitor_times: Optional[Sequence[float]]) -> List[int]:

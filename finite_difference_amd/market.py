@@ -88,23 +88,44 @@ def year_fraction(day_count: str, start: _dt.date, end: _dt.date) -> float:
 # ---------------------------------------------------------------------------
 
 
+_MAP_CACHE: Dict[tuple, Dict[str, float]] = {}
+
+
 class NacaCurve:
     """Date -> NACA lookup over a DataFrame with columns "Date" (ISO) / "NACA".
 
     Same semantics as the reference's row filter (exact ISO match, first row
     wins, missing date raises ValueError) with an O(1) dict instead of a scan.
+    A batch of trades usually shares one curve: the map is cached by the
+    curve's content (every date string and every NACA bit pattern), so each
+    pricer pays a fingerprint, not a rebuild.
     """
 
     def __init__(self, df):
         self.df = df
         self._map: Optional[Dict[str, float]] = None
 
+    def _build(self) -> Dict[str, float]:
+        col = self.df["Date"]
+        raw = col.to_numpy()
+        if raw.dtype == object and len(raw) and type(raw[0]) is str:
+            dates = tuple(raw.tolist())  # a column of date strings
+        else:
+            dates = tuple(col.astype(str).tolist())
+        naca = np.ascontiguousarray(self.df["NACA"].to_numpy(dtype=np.float64))
+        key = (dates, naca.tobytes())
+        m = _MAP_CACHE.get(key)
+        if m is None:
+            # reversed, so the first row of a repeated date wins
+            m = dict(zip(reversed(dates), reversed(naca.tolist())))
+            if len(_MAP_CACHE) > 64:
+                _MAP_CACHE.clear()
+            _MAP_CACHE[key] = m
+        return m
+
     def naca(self, d: _dt.date) -> Optional[float]:
         if self._map is None:
-            m: Dict[str, float] = {}
-            for k, v in zip(self.df["Date"].astype(str).tolist(), self.df["NACA"].tolist()):
-                m.setdefault(k, float(v))
-            self._map = m
+            self._map = self._build()
         return self._map.get(d.isoformat())
 
 

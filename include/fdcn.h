@@ -151,6 +151,15 @@ int fdcn_plan(int32_t B, int32_t n_nodes, int32_t n_time, int32_t it_mode, int32
 int fdcn_sm_extent(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                    const double* params);
 
+/* ---- host-side plan helpers (no device) -------------------------------- */
+/* Uniform log grid of the pricers' _build_log_grid
+ * (discrete_barrier_fdm_pricer.py:342-364, fd_american_equity.py:363-384):
+ *   x[i] = x_min + (double)i * dx,   s[i] = exp(x[i]),   i = 0..n
+ * with the C library's exp (the one CPython's math.exp calls), so the nodes
+ * are bit-identical to the reference's list comprehensions.  x may be NULL.
+ * Returns FDCN_OK or FDCN_EINVAL (n < 0, s NULL). */
+int fdcn_log_grid(double x_min, double dx, int32_t n, double* x, double* s);
+
 const char* fdcn_last_error(void);
 int fdcn_device_count(void);   /* gfx950 devices visible; 0 if none          */
 int fdcn_abi_version(void);    /* FDCN_ABI_VERSION                           */

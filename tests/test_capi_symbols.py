@@ -37,3 +37,19 @@ def test_invalid_size_reports_error():
     import pytest
     with pytest.raises(capi.FdcnError):
         capi.plan(3, False)
+
+
+def test_log_grid_is_bitwise_math_exp():
+    """fdcn_log_grid (host helper) reproduces the reference's
+    [math.exp(x_min + i*dx) for i in range(n+1)] bit for bit."""
+    import math
+    import numpy as np
+    rng = np.random.default_rng(5)
+    for _ in range(20):
+        x_min = float(rng.uniform(-2.0, 6.0))
+        dx = float(rng.uniform(1e-5, 1e-2))
+        n = int(rng.integers(1, 5000))
+        x, s = capi.log_grid(x_min, dx, n)
+        ref_x = [x_min + i * dx for i in range(n + 1)]
+        assert x.tolist() == ref_x
+        assert s.tolist() == list(map(math.exp, ref_x))
