@@ -265,8 +265,13 @@ __host__ __device__ inline int lds_doubles_per_scen(int lz) {
          (W > 1 ? Xch<W>::kSize : 0);
 }
 
+#ifdef FDCN_WAVES_PER_EU  // A/B builds only: occupancy target for the W=1 variants
+#define FDCN_OCC_ATTR __attribute__((amdgpu_waves_per_eu(W == 1 ? FDCN_WAVES_PER_EU : 1)))
+#else
+#define FDCN_OCC_ATTR
+#endif
 template <int IT, int W, int NPT, int ZG = 0>
-__global__ void __launch_bounds__(64 * W)
+__global__ void __launch_bounds__(64 * W) FDCN_OCC_ATTR
 fdcn_march(KArgs A) {
   constexpr int L = Geo<IT, W, NPT, ZG>::L;
   constexpr int SPB = Geo<IT, W, NPT, ZG>::SPB;
@@ -328,7 +333,12 @@ fdcn_march(KArgs A) {
   // recurrences run the S sub-chains interleaved (independent FMA chains) and
   // join them with a short Horner step in fm^M / bm^M, so a wave keeps S
   // fp64 FMAs in flight instead of one dependent chain.
+#ifdef FDCN_SUBCHAINS  // A/B builds only
+  constexpr int S = (NPT % FDCN_SUBCHAINS == 0 && NPT >= 4 * FDCN_SUBCHAINS) ? FDCN_SUBCHAINS
+                    : ((NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1));
+#else
   constexpr int S = (NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1);
+#endif
   constexpr int M = NPT / S;
 
   // ---- per-theta constants: scan window products + SM table -------------
