@@ -374,62 +374,83 @@ class AmericanFDMPricer:
         for k, v in st.items():
             setattr(self, k, v)
 
-    def prefetch(self, requests: Sequence[Tuple[float, int]]) -> None:
-        """Solve the (sigma, n_time) grids not yet cached, all together.
-
-        Segments are marched in lock-step: every pending request's segment i
-        goes into one batched launch (grouped by step count), then the host
-        applies the dividend jump, then segment i+1."""
-        pending = []
-        seen = set()
+    def _pending_jobs(self, requests: Sequence[Tuple[float, int]]) -> list:
+        """Grid jobs (one per uncached (sigma, n_time)) with their segments."""
+        pending, seen = [], set()
         for sig, nt in requests:
             key = self._state_key(sig, nt)
             if key in self._cache or key in seen:
                 continue
             seen.add(key)
             pending.append((key, float(sig), int(nt)))
-        if not pending:
-            return
-        sigma0 = self.sigma
-        saved = self._grid_state()
         jobs = []
+        if not pending:
+            return jobs
+        sigma0, saved = self.sigma, self._grid_state()
         try:
             for key, sig, nt in pending:
                 self.sigma = sig
                 self._build_log_grid()
                 divs, pts, steps = self._segments(nt)
-                jobs.append(dict(key=key, sigma=sig, grid=self._grid_state(), divs=divs,
-                                 pts=pts, steps=steps, v=self._payoff_array()))
-            n_seg = max(len(j["steps"]) for j in jobs)
-            for seg in range(n_seg):
-                solves, owners = [], []
-                for j in jobs:
-                    if seg >= len(j["steps"]):
-                        continue
-                    self.sigma = j["sigma"]
-                    self._restore(j["grid"])
-                    restart = seg == 0 or (seg > 0 and self.option_type == "call")
-                    ns = j["steps"][seg]
-                    if ns < 1:
-                        continue
-                    solves.append(self._segment_solve(j["v"], j["pts"][seg], j["pts"][seg + 1],
-                                                      ns, restart))
-                    owners.append(j)
-                if solves:
-                    if len(self.s_nodes) - 1 < 2:
-                        raise RuntimeError("Spatial grid too coarse.")
-                    for j, v in zip(owners, self._engine().run(solves)):
-                        j["v"] = v
-                for j in jobs:
-                    if seg < len(j["divs"]):
-                        self.sigma = j["sigma"]
-                        self._restore(j["grid"])
-                        j["v"] = self._apply_dividend_jump(j["v"], j["divs"][seg][1])
-            for j in jobs:
-                self._cache[j["key"]] = (np.asarray(j["v"], dtype=np.float64), j["grid"])
+                jobs.append(dict(owner=self, key=key, sigma=sig, grid=self._grid_state(),
+                                 divs=divs, pts=pts, steps=steps, v=self._payoff_array()))
         finally:
             self.sigma = sigma0
             self._restore(saved)
+        return jobs
+
+    @staticmethod
+    def _march_jobs(jobs: list, engine: Engine) -> None:
+        """March grid jobs of any number of trades in segment lock-step: every
+        job's segment i goes into one engine.run (one launch per distinct
+        (n_nodes, n_time)), then each job's dividend jump, then segment i+1;
+        finally each job's value vector is cached on its owner."""
+        if not jobs:
+            return
+        n_seg = max(len(j["steps"]) for j in jobs)
+        for seg in range(n_seg):
+            solves, owners = [], []
+            for j in jobs:
+                if seg >= len(j["steps"]) or j["steps"][seg] < 1:
+                    continue
+                p = j["owner"]
+                sigma0, saved = p.sigma, p._grid_state()
+                try:
+                    p.sigma = j["sigma"]
+                    p._restore(j["grid"])
+                    if len(p.s_nodes) - 1 < 2:
+                        raise RuntimeError("Spatial grid too coarse.")
+                    restart = seg == 0 or (seg > 0 and p.option_type == "call")
+                    solves.append(p._segment_solve(j["v"], j["pts"][seg], j["pts"][seg + 1],
+                                                   j["steps"][seg], restart))
+                finally:
+                    p.sigma = sigma0
+                    p._restore(saved)
+                owners.append(j)
+            if solves:
+                for j, v in zip(owners, engine.run(solves)):
+                    j["v"] = v
+            for j in jobs:
+                if seg < len(j["divs"]):
+                    p = j["owner"]
+                    sigma0, saved = p.sigma, p._grid_state()
+                    try:
+                        p.sigma = j["sigma"]
+                        p._restore(j["grid"])
+                        j["v"] = p._apply_dividend_jump(j["v"], j["divs"][seg][1])
+                    finally:
+                        p.sigma = sigma0
+                        p._restore(saved)
+        for j in jobs:
+            j["owner"]._cache[j["key"]] = (np.asarray(j["v"], dtype=np.float64), j["grid"])
+
+    def prefetch(self, requests: Sequence[Tuple[float, int]]) -> None:
+        """Solve the (sigma, n_time) grids not yet cached, all together.
+
+        Segments are marched in lock-step: every pending request's segment i
+        goes into one batched launch (grouped by step count), then the host
+        applies the dividend jump, then segment i+1."""
+        self._march_jobs(self._pending_jobs(requests), self._engine())
 
     def _solve_grid(self, n_time: Optional[int] = None) -> List[float]:
         """Value vector at valuation (fd_american_equity.py:778-843)."""
@@ -543,32 +564,15 @@ def prefetch_many(pricers: Sequence[AmericanFDMPricer], dv_sigma: float = 0.01,
                   use_richardson: bool = True) -> None:
     """Solve every grid that price_log2 + greeks_log2 of many trades will need.
 
-    Trades without dividends are a single segment each: all their unique
-    (sigma, n_time) grids go into one engine.run (one launch per distinct
-    (n_nodes, n_time)).  Trades with dividends are prefetched per trade
-    (segment lock-step across that trade's grids)."""
+    All trades' unique (sigma, n_time) grids are marched together in
+    segment lock-step (AmericanFDMPricer._march_jobs): trades without
+    dividends are one segment, so the whole set is one engine.run (one launch
+    per distinct (n_nodes, n_time)); trades with dividends add one round per
+    extra segment, shared by every trade, with the host's spline jumps in
+    between."""
     if not pricers:
         return
-    engine = pricers[0]._engine()
-    solves, owners = [], []
+    jobs = []
     for p in pricers:
-        if p._div_times_tau():
-            p.prefetch(p.greeks_requests(dv_sigma, use_richardson))
-            continue
-        sigma0, saved = p.sigma, p._grid_state()
-        seen = set()
-        for sig, nt in p.greeks_requests(dv_sigma, use_richardson):
-            key = p._state_key(sig, nt)
-            if key in p._cache or key in seen:
-                continue
-            seen.add(key)
-            p.sigma = sig
-            p._build_log_grid()
-            solves.append(p._segment_solve(p._payoff_array(), 0.0, p.time_to_expiry,
-                                           int(nt), True))
-            owners.append((p, key, p._grid_state()))
-        p.sigma = sigma0
-        p._restore(saved)
-    if solves:
-        for (p, key, grid), v in zip(owners, engine.run(solves)):
-            p._cache[key] = (np.asarray(v, dtype=np.float64), grid)
+        jobs.extend(p._pending_jobs(p.greeks_requests(dv_sigma, use_richardson)))
+    AmericanFDMPricer._march_jobs(jobs, pricers[0]._engine())

@@ -59,3 +59,24 @@ def test_batched_prefetch_matches_and_dedups():
     # no-dividend trades were solved in the single batched round
     assert eng.launches == launches
     assert launches >= 1 and len(nodiv) > 0
+
+
+def test_dividend_trades_share_lockstep_launches():
+    """Trades with dividends are marched together: segment i of every trade's
+    grids goes into the same engine.run, so the number of launches is set by
+    the grid shapes per segment round, not by the number of trades."""
+    eng = oracle_engine()
+    div_cases = [c for c in CASES if c["inputs"]["divs"]]
+    ps = [make(c, eng) for c in div_cases] + [make(c, eng) for c in div_cases]
+    before = eng.launches
+    prefetch_many(ps)
+    used = eng.launches - before
+    for p, c in zip(ps, div_cases + div_cases):
+        assert p.price_log2() == c["price_log2"]
+        assert p.greeks_log2() == c["greeks_log2"]
+    assert eng.launches - before == used  # everything came from the prefetch
+    solo = oracle_engine()
+    for c in div_cases:
+        q = make(c, solo)
+        prefetch_many([q])
+    assert used < solo.launches * 2  # two copies of each trade cost less than two solo runs
