@@ -17,6 +17,9 @@ Other workloads (--workload, same JSON line format):
   double   configs[4]: double knock-out call of double _barrier.py:139-146 on a
            4096 x 8192 grid, projection every step; --batch B sweeps sigma and
            the barriers (B=1 is the single-solve latency case).
+  analytic SURVEY §8(f) row 4, not a BASELINE config: 2^20 Reiner-Rubinstein
+           barrier contracts (barrier_engine.py) per launch, one GPU thread
+           each; its own metric line (contracts/s).
 
 value = total node-steps (configured nodes x steps x B x ranks) / max-over-
 ranks wall time of the K timed launches.
@@ -47,7 +50,7 @@ FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec sheet, FP64 vector
 # algorithmic bytes / flops per node-step
 BYTES_PER_NODE_STEP = {True: 32, False: 16}   # IT: V and lambda in+out; CN: V in+out
 FLOPS_PER_NODE_STEP = {True: 17, False: 10}   # RHS 5 (+2 lambda) + Thomas 5 (+ IT 5)
-DEFAULT_BATCH = {"american": 4096, "barrier": 10000, "double": 2048}
+DEFAULT_BATCH = {"american": 4096, "barrier": 10000, "double": 2048, "analytic": 1 << 20}
 
 
 def parse():
@@ -199,8 +202,87 @@ def load_traffic(workload: str):
         return None
 
 
+def bench_analytic(args):
+    """Closed-form barrier batch (fdcn_rr_barrier_batch_dev): contracts/s."""
+    import numpy as np
+    import torch
+    from finite_difference_amd import capi
+    from finite_difference_amd.analytic import BarrierEngine, _rr_encode
+    capi.require_device()
+    dev = torch.device("cuda", 0)
+    B = args.batch or DEFAULT_BATCH["analytic"]
+    rng = np.random.default_rng(20250728)
+    s = rng.uniform(50, 150, B)
+    up = rng.integers(0, 2, B).astype(bool)
+    P = np.stack([s, rng.uniform(-0.02, 0.08, B), rng.uniform(0.0, 0.1, B),
+                  rng.uniform(0.05, 2.0, B), s * rng.uniform(0.7, 1.3, B),
+                  rng.uniform(0.1, 0.6, B),
+                  s * np.where(up, rng.uniform(1.02, 1.4, B), rng.uniform(0.6, 0.98, B)),
+                  rng.uniform(0.0, 3.0, B)], axis=1)
+    F = np.zeros((B, capi.RR_NFLAG), dtype=np.int32)
+    F[:, 0] = np.arange(B) % 2
+    F[:, 1] = np.where(up, 0, 1)
+    F[:, 2] = (np.arange(B) // 2) % 2
+    dP = torch.from_numpy(P).to(dev)
+    dF = torch.from_numpy(F).to(dev)
+    price = torch.empty(B, dtype=torch.float64, device=dev)
+    van = torch.empty(B, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        capi._check(capi.lib().fdcn_rr_barrier_batch_dev(B, dP.data_ptr(), dF.data_ptr(),
+                                                         price.data_ptr(), van.data_ptr(),
+                                                         stream.cuda_stream))
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
+    got = price.cpu().numpy()
+    cpu = None
+    if not args.no_cpu_baseline:  # the host engine (Python/NumPy/SciPy), one core
+        n, t_cpu = 0, 0.0
+        names = ("s", "b", "r", "t", "x", "sigma", "h", "k")
+        while t_cpu < min(args.cpu_seconds, 5.0) and n < B:
+            c = dict(zip(names, map(float, P[n])))
+            c.update(optionflag="cp"[F[n, 0]], directionflag="ud"[F[n, 1]],
+                     in_out_flag="io"[F[n, 2]])
+            t1 = time.perf_counter()
+            ref = BarrierEngine(**c).price()
+            t_cpu += time.perf_counter() - t1
+            assert abs(ref - got[n]) <= 1e-11 * abs(ref) + 1e-12, (n, ref, got[n])
+            n += 1
+        cpu = {"value": n / t_cpu, "unit": "contracts/s", "cores": 1, "kind": "port",
+               "sample": f"first {n} contracts through analytic.BarrierEngine (host, "
+                         f"NumPy/SciPy, the reference's formulas), each checked against "
+                         f"the GPU result"}
+    bytes_per = 8 * capi.RR_NPARAM + 4 * capi.RR_NFLAG + 16
+    gbs = bytes_per * B / (kernel_ms * 1e-3) / 1e9
+    print(json.dumps({
+        "metric": "closed-form barrier contracts/s (Reiner-Rubinstein, barrier_engine.py)",
+        "value": B * args.steps / elapsed, "unit": "contracts/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (uniform spot/strike/barrier/vol/rate/tenor sweep)",
+        "config": {"workload": f"rr_barrier_batch{B}", "contracts": B},
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs / HBM_PEAK_GBS, "traffic": None},
+        "kernel_ms_per_launch": kernel_ms, "outputs_finite": bool(np.all(np.isfinite(got))),
+        "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "analytic":
+        return bench_analytic(args)
     import numpy as np
     import torch
     import torch.distributed as dist

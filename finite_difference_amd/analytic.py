@@ -10,6 +10,9 @@ the hot path and the cross-checks for the FD kernels.
   the log-barrier l; that is kept by default for parity
   (``corrected_put=False``) and fixed with ``corrected_put=True``.
 * ``black_scholes``: generalized Black-Scholes with carry b.
+* ``barrier_engine_batch`` / ``double_barrier_batch``: the same two engines
+  for many contracts at once, one GPU thread per contract (libfdcn
+  ``fdcn_rr_barrier_batch`` / ``fdcn_double_barrier_batch``).
 """
 from __future__ import annotations
 
@@ -203,3 +206,52 @@ class DoubleBarrier:
         if self.inflag == "in":
             return bs - out
         raise ValueError("Incorrect inflag")
+
+
+def _rr_encode(optionflag, directionflag, in_out_flag, barrier_status=None,
+               rebate_timing_in=None, rebate_timing_out=None):
+    if optionflag.lower() not in ("c", "p") or directionflag.lower() not in ("u", "d") or \
+            in_out_flag.lower() not in ("i", "o"):
+        raise ValueError("flags must be optionflag c/p, directionflag u/d, in_out_flag i/o")
+    if barrier_status not in (None, "crossed", "not_crossed"):
+        raise ValueError("barrier_status must be None, 'crossed', or 'not_crossed'.")
+    bits = (1 if _norm_rebate_timing(rebate_timing_in, "expiry") == "hit" else 0) | \
+        (2 if _norm_rebate_timing(rebate_timing_out, "hit") == "expiry" else 0)
+    return [0 if optionflag.lower() == "c" else 1, 0 if directionflag.lower() == "u" else 1,
+            0 if in_out_flag.lower() == "i" else 1, 1 if barrier_status == "crossed" else 0,
+            bits]
+
+
+def barrier_engine_batch(contracts):
+    """BarrierEngine(**c).price() / .vanilla() for every dict ``c`` in
+    ``contracts`` (BarrierEngine's keyword names), on the GPU.
+    Returns (price, vanilla) arrays."""
+    from . import capi
+    P = np.empty((len(contracts), capi.RR_NPARAM), dtype=np.float64)
+    F = np.empty((len(contracts), capi.RR_NFLAG), dtype=np.int32)
+    for i, c in enumerate(contracts):
+        if float(c["sigma"]) <= 0 or float(c["t"]) <= 0:
+            raise ValueError("sigma and t must be positive.")
+        P[i] = (c["s"], c["b"], c["r"], c["t"], c["x"], c["sigma"], c["h"], c["k"])
+        F[i] = _rr_encode(c["optionflag"], c["directionflag"], c["in_out_flag"],
+                          c.get("barrier_status"), c.get("rebate_timing_in"),
+                          c.get("rebate_timing_out"))
+    return capi.rr_barrier_batch(P, F)
+
+
+def double_barrier_batch(contracts, m: int = 4):
+    """DoubleBarrier(S, X, L, U, sigma, callflag, inflag, m,
+    corrected_put).price(b, r, T) for every dict in ``contracts``, on the GPU."""
+    from . import capi
+    P = np.empty((len(contracts), capi.DB_NPARAM), dtype=np.float64)
+    F = np.empty((len(contracts), capi.DB_NFLAG), dtype=np.int32)
+    for i, c in enumerate(contracts):
+        cf, io = c["callflag"].lower(), c["inflag"].lower()
+        if cf not in ("c", "p"):
+            raise ValueError("Incorrect callflag (use 'c' or 'p')")
+        if io not in ("in", "out"):
+            raise ValueError("Incorrect inflag")
+        P[i] = (c["S"], c["X"], c["L"], c["U"], c["sigma"], c["b"], c["r"], c["T"])
+        F[i] = (0 if cf == "c" else 1, 0 if io == "in" else 1,
+                1 if c.get("corrected_put", False) else 0)
+    return capi.double_barrier_batch(P, F, m)

@@ -31,8 +31,12 @@ NIPARAM = 7
 ABI_VERSION = 3
 
 EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batch_dev",
-            "fdcn_plan", "fdcn_sm_extent", "fdcn_log_grid", "fdcn_last_error",
-            "fdcn_device_count", "fdcn_abi_version")
+            "fdcn_plan", "fdcn_sm_extent", "fdcn_log_grid", "fdcn_rr_barrier_batch",
+            "fdcn_rr_barrier_batch_dev", "fdcn_double_barrier_batch",
+            "fdcn_double_barrier_batch_dev", "fdcn_last_error", "fdcn_device_count",
+            "fdcn_abi_version")
+RR_NPARAM, RR_NFLAG = 8, 5
+DB_NPARAM, DB_NFLAG = 8, 3
 
 
 class FdcnError(RuntimeError):
@@ -74,6 +78,14 @@ def lib() -> ctypes.CDLL:
             L.fdcn_sm_extent.argtypes = [_I, _I, _I, _I, _PD]
             L.fdcn_log_grid.restype = _I
             L.fdcn_log_grid.argtypes = [ctypes.c_double, ctypes.c_double, _I, _V, _V]
+            L.fdcn_rr_barrier_batch.restype = _I
+            L.fdcn_rr_barrier_batch.argtypes = [_I, _V, _V, _V, _V]
+            L.fdcn_rr_barrier_batch_dev.restype = _I
+            L.fdcn_rr_barrier_batch_dev.argtypes = [_I, _V, _V, _V, _V, _V]
+            L.fdcn_double_barrier_batch.restype = _I
+            L.fdcn_double_barrier_batch.argtypes = [_I, _I, _V, _V, _V]
+            L.fdcn_double_barrier_batch_dev.restype = _I
+            L.fdcn_double_barrier_batch_dev.argtypes = [_I, _I, _V, _V, _V, _V]
             L.fdcn_last_error.restype = ctypes.c_char_p
             L.fdcn_last_error.argtypes = []
             L.fdcn_device_count.restype = ctypes.c_int
@@ -183,3 +195,34 @@ def log_grid(x_min: float, dx: float, n: int):
     s = np.empty(n + 1, dtype=np.float64)
     _check(lib().fdcn_log_grid(float(x_min), float(dx), int(n), x.ctypes.data, s.ctypes.data))
     return x, s
+
+
+def rr_barrier_batch(params, flags):
+    """Reiner-Rubinstein barrier batch on the GPU -> (price[B], vanilla[B]).
+    params [B, RR_NPARAM] = s, b, r, t, x, sigma, h, k; flags [B, RR_NFLAG]."""
+    require_device()
+    P = _f64(params).reshape(-1, RR_NPARAM)
+    F = _i32(flags).reshape(-1, RR_NFLAG)
+    if P.shape[0] != F.shape[0]:
+        raise ValueError("params and flags disagree on B")
+    B = P.shape[0]
+    price = np.empty(B, dtype=np.float64)
+    vanilla = np.empty(B, dtype=np.float64)
+    _check(lib().fdcn_rr_barrier_batch(B, P.ctypes.data, F.ctypes.data, price.ctypes.data,
+                                       vanilla.ctypes.data))
+    return price, vanilla
+
+
+def double_barrier_batch(params, flags, m: int = 4):
+    """Double-barrier (Douady series) batch on the GPU -> price[B].
+    params [B, DB_NPARAM] = S, X, L, U, sigma, b, r, T; flags [B, DB_NFLAG]."""
+    require_device()
+    P = _f64(params).reshape(-1, DB_NPARAM)
+    F = _i32(flags).reshape(-1, DB_NFLAG)
+    if P.shape[0] != F.shape[0]:
+        raise ValueError("params and flags disagree on B")
+    B = P.shape[0]
+    price = np.empty(B, dtype=np.float64)
+    _check(lib().fdcn_double_barrier_batch(B, int(m), P.ctypes.data, F.ctypes.data,
+                                           price.ctypes.data))
+    return price

@@ -1346,6 +1346,11 @@ int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ran
 
 }  // namespace
 
+namespace fdcn_internal {
+// error reporting shared with the other translation units of libfdcn
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+}  // namespace fdcn_internal
+
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------

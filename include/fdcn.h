@@ -151,6 +151,38 @@ int fdcn_plan(int32_t B, int32_t n_nodes, int32_t n_time, int32_t it_mode, int32
 int fdcn_sm_extent(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                    const double* params);
 
+/* ---- batched closed-form barrier engines (one thread per contract) ------ */
+/* Reiner-Rubinstein single continuous barrier with cash rebate and barrier
+ * status; replaces BarrierEngine(s,b,r,t,x,sigma,h,optionflag,directionflag,
+ * in_out_flag,k,barrier_status,rebate_timing_in,rebate_timing_out).price() /
+ * .vanilla() (barrier_engine.py:38-44, 189) for B contracts at once.
+ *   params[B][FDCN_RR_NPARAM] = s, b, r, t, x (strike), sigma, h (barrier), k (rebate)
+ *   flags [B][FDCN_RR_NFLAG]  = option (0 call, 1 put), direction (0 up, 1 down),
+ *                               in/out (0 in, 1 out), status (0 not crossed, 1 crossed),
+ *                               rebate timing bits (1: knock-in rebate paid at hit,
+ *                               2: knock-out rebate paid at expiry; defaults 0)
+ *   price[B], vanilla[B] (the A factor).  */
+#define FDCN_RR_NPARAM 8
+#define FDCN_RR_NFLAG 5
+int fdcn_rr_barrier_batch(int32_t B, const double* params, const int32_t* flags,
+                          double* price, double* vanilla);
+int fdcn_rr_barrier_batch_dev(int32_t B, const double* params, const int32_t* flags,
+                              double* price, double* vanilla, void* stream);
+
+/* Double knock-out / knock-in (Ikeda-Kunitomo / Douady series, n = -m..m);
+ * replaces DoubleBarrier(S,X,L,U,sigma,callflag,inflag,m).price(b,r,T)
+ * (double _barrier.py:33-134).
+ *   params[B][FDCN_DB_NPARAM] = S, X, L, U, sigma, b, r, T
+ *   flags [B][FDCN_DB_NFLAG]  = option (0 call, 1 put), in/out (0 in, 1 out),
+ *                               corrected put (0: the reference's alpha = 1, :95)
+ *   price[B]. */
+#define FDCN_DB_NPARAM 8
+#define FDCN_DB_NFLAG 3
+int fdcn_double_barrier_batch(int32_t B, int32_t m, const double* params,
+                              const int32_t* flags, double* price);
+int fdcn_double_barrier_batch_dev(int32_t B, int32_t m, const double* params,
+                                  const int32_t* flags, double* price, void* stream);
+
 /* ---- host-side plan helpers (no device) -------------------------------- */
 /* Uniform log grid of the pricers' _build_log_grid
  * (discrete_barrier_fdm_pricer.py:342-364, fd_american_equity.py:363-384):

@@ -7,4 +7,5 @@ NAME=$1; shift
 cd "$(dirname "$0")/.."
 mkdir -p build/ab/$NAME
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
-  -o build/ab/$NAME/libfdcn.so finite_difference_amd/csrc/fdcn_kernels.hip
+  -o build/ab/$NAME/libfdcn.so finite_difference_amd/csrc/fdcn_kernels.hip \
+  finite_difference_amd/csrc/fdcn_analytic.hip
