@@ -308,16 +308,32 @@ fdcn_march(KArgs A) {
   // registers are live) into this wave's workspace row: lane l owns steps
   // m = l (mod 64) and is the only lane that reads them back, so no
   // synchronisation is needed.  tau_m = tau0 + (m+1) dt (…pricer.py:519).
+  // IT: what the step needs is not the Dirichlet value itself but its
+  // theta-form rhs term (-A_L)(lo_m + c2 lo_{m-1}) / (-A_U)(hi_m + c2 hi_{m-1})
+  // (see the IT rhs below); IT has no knock-out, so lo_{m-1} is simply the
+  // previous step's value and the whole term is tabulated here.
   double2* bnd = reinterpret_cast<double2*>(A.bnd) + ((size_t)scen * W + wave) * A.n_pad;
+  const int lof = uni_i(I[FDCN_I_LO_FORM]), hif = uni_i(I[FDCN_I_HI_FORM]);
+  const double l0 = uni(P[FDCN_P_LO_C0]), l1 = uni(P[FDCN_P_LO_E0]), l2 = uni(P[FDCN_P_LO_C1]),
+               l3 = uni(P[FDCN_P_LO_E1]);
+  const double h0 = uni(P[FDCN_P_HI_C0]), h1 = uni(P[FDCN_P_HI_E0]), h2 = uni(P[FDCN_P_HI_C1]),
+               h3 = uni(P[FDCN_P_HI_E1]);
   {
-    const int lof = uni_i(I[FDCN_I_LO_FORM]), hif = uni_i(I[FDCN_I_HI_FORM]);
-    const double l0 = uni(P[FDCN_P_LO_C0]), l1 = uni(P[FDCN_P_LO_E0]),
-                 l2 = uni(P[FDCN_P_LO_C1]), l3 = uni(P[FDCN_P_LO_E1]);
-    const double h0 = uni(P[FDCN_P_HI_C0]), h1 = uni(P[FDCN_P_HI_E0]),
-                 h2 = uni(P[FDCN_P_HI_C1]), h3 = uni(P[FDCN_P_HI_E1]);
+    const double* vb = A.v_init + (size_t)scen * n_nodes;
+    const double v_lo0 = IT ? uni(vb[0]) : 0.0, v_hi0 = IT ? uni(vb[n_nodes - 1]) : 0.0;
     for (int m = lane; m < A.n_pad; m += 64) {
       const double tau = tau0 + (double)(m + 1) * dt;
-      bnd[m] = make_double2(bnd_eval(lof, l0, l1, l2, l3, tau), bnd_eval(hif, h0, h1, h2, h3, tau));
+      const double lo = bnd_eval(lof, l0, l1, l2, l3, tau), hi = bnd_eval(hif, h0, h1, h2, h3, tau);
+      if constexpr (IT) {
+        const double tp = tau0 + (double)m * dt;
+        const double lo_p = m == 0 ? v_lo0 : bnd_eval(lof, l0, l1, l2, l3, tp);
+        const double hi_p = m == 0 ? v_hi0 : bnd_eval(hif, h0, h1, h2, h3, tp);
+        const double th = m < A.n_ranna ? 1.0 : 0.5;
+        const double c2 = (1.0 - th) / th;  // Phase::c2, pl, pu for this step's theta
+        bnd[m] = make_double2((th * dt * ca) * fma(c2, lo_p, lo), (th * dt * cc) * fma(c2, hi_p, hi));
+      } else {
+        bnd[m] = make_double2(lo, hi);
+      }
     }
   }
 
@@ -326,6 +342,11 @@ fdcn_march(KArgs A) {
   const int L_short = L_act * NPT - n_int;
   const bool active = t < L_act;
   const bool shrt = t < L_short;
+  // 1.0 on the lane that holds interior node 0 / the last interior node
+  const double e_first = (t == 0) ? 1.0 : 0.0;
+  const double e_last = (t == L_act - 1) ? 1.0 : 0.0;
+  (void)e_first;
+  (void)e_last;
   const int s_t = t * NPT - (t < L_short ? t : L_short);  // first interior index
 
   // ---- chunk decomposition for instruction-level parallelism -------------
@@ -478,8 +499,8 @@ fdcn_march(KArgs A) {
         if (v < wave) cw = fma(xch[Xch<W>::kFtot + v], cw, xch[Xch<W>::kFB + v]);
       b = fma(Fpre, cw, b);
     }
-    double cin = shfl_up1(b, 1);
-    if (lane == 0) cin = cw;
+    double cin = shfl_up1(b, 1);  // DPP bound_ctrl: lane 0 receives 0 (= cw for W = 1)
+    if (W > 1 && lane == 0) cin = cw;
     if (!active) cin = 0.0;
     FDCN_STAMP(st_acc, st_prev, 3);
     // forward pass 2: carries into every sub-chain, then S chains in parallel
@@ -530,8 +551,8 @@ fdcn_march(KArgs A) {
         if (v > wave) cwb = fma(xch[Xch<W>::kGtot + v], cwb, xch[Xch<W>::kBC + v]);
       cb = fma(Gsuf, cwb, cb);
     }
-    double cinb = shfl_dn1(cb, 1);
-    if (lane == 63) cinb = cwb;
+    double cinb = shfl_dn1(cb, 1);  // lane 63 receives 0 (= cwb for W = 1)
+    if (W > 1 && lane == 63) cinb = cwb;
     if (!active) cinb = 0.0;
     FDCN_STAMP(st_acc, st_prev, 6);
     c[S - 1] = cinb;
@@ -711,6 +732,9 @@ fdcn_march(KArgs A) {
   // phase for step 0 (ph currently holds the theta the last table was built for)
   double smc;
   int tab;
+  // this lane's row of the correction tables (lanes >= lz read row lz-1)
+  const int zoff_r = (t < lz ? t : lz - 1) * (NPT + 1);
+  const int zoff_c = zoff_r + lz * (NPT + 1);
   if (use_r) {
     smc = smc_r;
     tab = 0;
@@ -758,12 +782,12 @@ fdcn_march(KArgs A) {
       // plus (-A_L)(lo_new + c2 lo_old) at node 0 and (-A_U)(hi_new + c2
       // hi_old) at the last node.  The rhs is pointwise: no stencil and no
       // neighbour exchange.  Unscaled, so the solve returns r (x + c2 V).
-      const double blo = ph.pl * fma(ph.c2, V0, lo_new);
-      const double bhi = ph.pu * fma(ph.c2, VN, hi_new);
+      // blo / bhi come tabulated from the prologue (lo_new / hi_new hold them)
 #pragma unroll
       for (int k = 0; k < NPT; ++k) V[k] += QS[k];
-      if (t == 0) V[0] += blo;
-      if (t == L_act - 1) V[NPT - 1] += bhi;  // the last active lane is never short
+      V[0] = fma(e_first, lo_new, V[0]);            // + blo on the first lane
+      V[NPT - 1] = fma(e_last, hi_new, V[NPT - 1]);  // + bhi on the last (never short)
+      if (shrt) V[NPT - 1] = 0.0;                   // the phantom slot's rhs
     } else if constexpr (kSplit) {
       // theta form of the reference step A x = B V (+ Dirichlet terms,
       // discrete_barrier_fdm_pricer.py:531-537) with B = (I - (1-theta) A) /
@@ -862,7 +886,7 @@ fdcn_march(KArgs A) {
       }
       g = (t < lz) ? -(smc * y0) : 0.0;
       // lane-major rows, stride NPT+1: bank-spread, immediate offsets
-      zoff = opaque((tab * lz + (t < lz ? t : lz - 1)) * (NPT + 1));
+      zoff = opaque(tab ? zoff_c : zoff_r);
     }
     if constexpr (kSplit) {
       // x = s (T + g z) - c2 V: c2 = 1 for theta = 1/2; the Rannacher steps
@@ -955,17 +979,13 @@ fdcn_march(KArgs A) {
         }
       }
     }
-    if constexpr (IT) {
-      // the phantom slot of a short lane stays an exact zero (zero rhs)
-      if (shrt) {
-        V[NPT - 1] = 0.0;
-        QS[NPT - 1] = 0.0;
-      }
-    } else if constexpr (kSplit) {
+    if constexpr (kSplit) {
       if (shrt) V[NPT - 1] = 0.0;
     }
-    V0 = lo_new;
-    VN = hi_new;
+    if constexpr (!IT) {  // IT reads the tabulated terms instead
+      V0 = lo_new;
+      VN = hi_new;
+    }
     if (!IT && m + 1 == next_mon) {  // knock-out projection (uniform branch)
       const double reb = cur_reb;
       double rebv = reb;  // VGPR copy: v_cndmask takes the mask as its SGPR operand
@@ -1024,6 +1044,13 @@ fdcn_march(KArgs A) {
     atomicAdd(&fdcn_stamps[kNumStamps], 1ull);
   }
 #endif
+  if constexpr (IT) {  // Dirichlet values of the last step (the loop kept only rhs terms)
+    if (A.n_time > 0) {
+      const double tau = tau0 + (double)A.n_time * dt;
+      V0 = bnd_eval(lof, l0, l1, l2, l3, tau);
+      VN = bnd_eval(hif, h0, h1, h2, h3, tau);
+    }
+  }
   // ---- store ---------------------------------------------------------------
   double* vout = A.v_out + (size_t)scen * n_nodes;
   const double poison = overflow ? __longlong_as_double(0x7ff8000000000000ll) : 0.0;
