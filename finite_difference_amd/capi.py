@@ -31,7 +31,8 @@ NIPARAM = 7
 ABI_VERSION = 3
 
 EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batch_dev",
-            "fdcn_plan", "fdcn_sm_extent", "fdcn_log_grid", "fdcn_rr_barrier_batch",
+            "fdcn_plan", "fdcn_sm_extent", "fdcn_log_grid", "fdcn_dividend_jump",
+            "fdcn_rr_barrier_batch",
             "fdcn_rr_barrier_batch_dev", "fdcn_double_barrier_batch",
             "fdcn_double_barrier_batch_dev", "fdcn_last_error", "fdcn_device_count",
             "fdcn_abi_version")
@@ -78,6 +79,8 @@ def lib() -> ctypes.CDLL:
             L.fdcn_sm_extent.argtypes = [_I, _I, _I, _I, _PD]
             L.fdcn_log_grid.restype = _I
             L.fdcn_log_grid.argtypes = [ctypes.c_double, ctypes.c_double, _I, _V, _V]
+            L.fdcn_dividend_jump.restype = _I
+            L.fdcn_dividend_jump.argtypes = [_I, _V, _V, ctypes.c_double, ctypes.c_double, _V]
             L.fdcn_rr_barrier_batch.restype = _I
             L.fdcn_rr_barrier_batch.argtypes = [_I, _V, _V, _V, _V]
             L.fdcn_rr_barrier_batch_dev.restype = _I
@@ -226,3 +229,20 @@ def double_barrier_batch(params, flags, m: int = 4):
     _check(lib().fdcn_double_barrier_batch(B, int(m), P.ctypes.data, F.ctypes.data,
                                            price.ctypes.data))
     return price
+
+
+def dividend_jump(s_nodes, v, cash_div: float, strike_call: float = -1.0) -> np.ndarray:
+    """V(t_d-, S) = V(t_d+, S - D) through the natural cubic spline, and for
+    calls (strike_call >= 0) max with the payoff -- in libfdcn, bit-identical to
+    fd_american_equity.py:479-553/732-772 (host only, no device)."""
+    S = _f64(s_nodes)
+    V = _f64(v)
+    if S.shape != V.shape or S.ndim != 1:
+        raise ValueError("s_nodes and v must be 1-D arrays of the same length")
+    out = np.empty_like(V)
+    rc = lib().fdcn_dividend_jump(S.shape[0], S.ctypes.data, V.ctypes.data, float(cash_div),
+                                  float(strike_call), out.ctypes.data)
+    if rc != 0:
+        msg = lib().fdcn_last_error().decode(errors="replace")
+        raise ValueError(msg)
+    return out

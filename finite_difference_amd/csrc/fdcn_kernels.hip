@@ -45,7 +45,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <vector>
 
 #include "../../include/fdcn.h"
 
@@ -1455,6 +1457,52 @@ int fdcn_log_grid(double x_min, double dx, int32_t n, double* x, double* s) {
     const double xi = x_min + (double)i * dx;  // the reference's x_min + i * dx
     if (x) x[i] = xi;
     s[i] = ::exp(xi);                           // libm exp, as math.exp
+  }
+  return FDCN_OK;
+}
+
+int fdcn_dividend_jump(int32_t n, const double* s, const double* v, double cash_div,
+                       double strike_call, double* v_out) {
+#pragma clang fp contract(off)
+  if (n < 2 || !s || !v || !v_out) return fail(FDCN_EINVAL, "fdcn_dividend_jump: n >= 2 and non-NULL arrays");
+  for (int32_t i = 0; i + 1 < n; ++i)
+    if (!(s[i + 1] - s[i] > 0.0)) return fail(FDCN_EINVAL, "x must be strictly increasing.");
+  // natural cubic spline through (s, v): fd_american_equity.py:479-553
+  std::vector<double> h(n - 1), alpha(n, 0.0), l(n, 1.0), mu(n, 0.0), z(n, 0.0), c(n, 0.0),
+      b(n - 1, 0.0), d(n - 1, 0.0);
+  for (int32_t i = 0; i + 1 < n; ++i) h[i] = s[i + 1] - s[i];
+  for (int32_t i = 1; i + 1 < n; ++i)
+    alpha[i] = 3.0 / h[i] * (v[i + 1] - v[i]) - 3.0 / h[i - 1] * (v[i] - v[i - 1]);
+  for (int32_t i = 1; i + 1 < n; ++i) {
+    l[i] = 2.0 * (s[i + 1] - s[i - 1]) - h[i - 1] * mu[i - 1];
+    mu[i] = h[i] / l[i];
+    z[i] = (alpha[i] - h[i - 1] * z[i - 1]) / l[i];
+  }
+  for (int32_t j = n - 2; j >= 0; --j) {
+    c[j] = z[j] - mu[j] * c[j + 1];
+    b[j] = (v[j + 1] - v[j]) / h[j] - h[j] * (c[j + 1] + 2.0 * c[j]) / 3.0;
+    d[j] = (c[j + 1] - c[j]) / (3.0 * h[j]);
+  }
+  // V(t_d-, S) = V(t_d+, S - D) (:732-772); interval by searchsorted(side="right") - 1
+  for (int32_t i = 0; i < n; ++i) {
+    const double q = s[i] - cash_div;
+    double cont;
+    if (q <= s[0]) {
+      cont = v[0];
+    } else if (q >= s[n - 1]) {
+      cont = v[n - 1];
+    } else {
+      int32_t j = (int32_t)(std::upper_bound(s, s + n, q) - s) - 1;
+      if (j > n - 2) j = n - 2;
+      const double t = q - s[j];
+      cont = v[j] + b[j] * t + c[j] * t * t + d[j] * t * t * t;
+    }
+    if (strike_call >= 0.0) {  // calls may exercise at the ex-date: max(cont, payoff)
+      const double e = s[i] - strike_call;
+      const double ex = (0.0 > e) ? 0.0 : e;     // Python max(e, 0.0) (keeps e's zero sign)
+      cont = (ex > cont) ? ex : cont;            // Python max(cont, ex)
+    }
+    v_out[i] = cont;
   }
   return FDCN_OK;
 }

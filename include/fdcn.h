@@ -192,6 +192,16 @@ int fdcn_double_barrier_batch_dev(int32_t B, int32_t m, const double* params,
  * Returns FDCN_OK or FDCN_EINVAL (n < 0, s NULL). */
 int fdcn_log_grid(double x_min, double dx, int32_t n, double* x, double* s);
 
+/* Discrete-dividend jump between two American segments
+ * (AmericanFDMPricer._apply_dividend_jump, fd_american_equity.py:732-772,
+ * with the natural cubic spline of :479-553):
+ *   q_i = s_i - cash_div,  V_out[i] = v[0] if q_i <= s[0], v[n-1] if q_i >= s[n-1],
+ *   else spline(q_i);  calls (strike_call >= 0): V_out[i] = max(V_out[i], max(s_i - K, 0)).
+ * Same operation order as the reference, so the result is bit-identical.
+ * s strictly increasing, n >= 2.  Host only (no device). */
+int fdcn_dividend_jump(int32_t n, const double* s, const double* v, double cash_div,
+                       double strike_call, double* v_out);
+
 const char* fdcn_last_error(void);
 int fdcn_device_count(void);   /* gfx950 devices visible; 0 if none          */
 int fdcn_abi_version(void);    /* FDCN_ABI_VERSION                           */

@@ -80,3 +80,17 @@ def test_dividend_trades_share_lockstep_launches():
         q = make(c, solo)
         prefetch_many([q])
     assert used < solo.launches * 2  # two copies of each trade cost less than two solo runs
+
+
+def test_native_dividend_jump_is_bitwise_numpy():
+    """fdcn_dividend_jump (C, in libfdcn) equals the NumPy restatement of the
+    reference's spline jump bit for bit, puts and calls, several cash amounts."""
+    rng = np.random.default_rng(9)
+    for case in CASES:
+        p = make(case, oracle_engine())
+        p._build_log_grid()
+        v = np.sort(rng.uniform(0, 50, len(p.s_nodes)))[::-1].tolist()
+        for D in (0.0, 0.37, 1.5, 25.0):
+            a = p._apply_dividend_jump(v, D)
+            b = p._apply_dividend_jump_numpy(v, D)
+            assert [x.hex() for x in a] == [float(x).hex() for x in b], (case["name"], D)
