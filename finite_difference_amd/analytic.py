@@ -20,7 +20,11 @@ import math
 from typing import Dict, Optional
 
 import numpy as np
-from scipy.stats import norm
+from scipy.special import ndtr
+
+
+class norm:  # noqa: N801 - scipy.stats.norm.cdf is ndtr((x - 0) / 1); called directly
+    cdf = staticmethod(ndtr)
 
 
 def _norm_rebate_timing(s: Optional[str], default: str) -> str:

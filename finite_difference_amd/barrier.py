@@ -57,17 +57,36 @@ def tail_quantile() -> float:
     return _K_TAIL
 
 
+_MON_CACHE: Dict[tuple, frozenset] = {}
+
+
+def _nearest_interior(s: Sequence[float], x: float) -> int:
+    """1 + argmin_{1 <= i <= len(s)-2} |s_i - x| for increasing s (first
+    index on ties, as np.argmin), by bisection instead of a full scan."""
+    lo, hi = 1, len(s) - 2
+    j = bisect.bisect_left(s, x, lo, hi + 1)  # first i in [lo, hi+1) with s_i >= x
+    if j <= lo:
+        return lo
+    if j > hi:
+        return hi
+    return j - 1 if abs(s[j - 1] - x) <= abs(s[j] - x) else j
+
+
 def _norm_cdf(x: float) -> float:
-    from scipy.stats import norm
-    return float(norm.cdf(x))
+    """scipy.stats.norm.cdf(x), which evaluates scipy.special.ndtr((x - 0) / 1):
+    the same function called directly, without the frozen-distribution
+    argument handling (bit-identical, ~100x cheaper per scalar call)."""
+    from scipy.special import ndtr
+    return float(ndtr(x))
 
 
 class _Grid:
-    __slots__ = ("n_space", "n_time", "S_min", "S_max", "dx", "s_nodes")
+    __slots__ = ("n_space", "n_time", "S_min", "S_max", "dx", "s_nodes", "s_arr")
 
-    def __init__(self, n_space, n_time, S_min, S_max, dx, s_nodes):
+    def __init__(self, n_space, n_time, S_min, S_max, dx, s_nodes, s_arr=None):
         self.n_space, self.n_time = n_space, n_time
         self.S_min, self.S_max, self.dx, self.s_nodes = S_min, S_max, dx, s_nodes
+        self.s_arr = s_arr  # the same nodes as a float64 array
 
 
 class DiscreteBarrierFDMPricer:
@@ -320,8 +339,8 @@ class DiscreteBarrierFDMPricer:
         n = self.num_space_nodes
         dx = (x_max - x_min) / n
         # [math.exp(x_min + i * dx) for i in range(n + 1)] (:358), in libfdcn
-        s = capi.log_grid(x_min, dx, n)[1].tolist()
-        return _Grid(n, self.num_time_steps, self._S_min, self._S_max, dx, s)
+        s_arr = capi.log_grid(x_min, dx, n)[1]
+        return _Grid(n, self.num_time_steps, self._S_min, self._S_max, dx, s_arr.tolist(), s_arr)
 
     def _build_log_grid(self) -> float:
         g = self._grid()
@@ -350,12 +369,19 @@ class DiscreteBarrierFDMPricer:
         return Boundary(FORM_PROD, k, -r, s_nodes[0], b - r), Boundary()
 
     def _monitor_indices_tau(self, dt: float) -> set:
+        key = (dt, self.time_to_expiry, self.num_time_steps, tuple(self.monitor_times))
+        hit = _MON_CACHE.get(key)
+        if hit is not None:  # a scenario file shares its dates: computed once
+            return set(hit)
         idx = set()
         for t_mon in self.monitor_times:
             if t_mon <= 0.0 or t_mon > self.time_to_expiry:
                 continue
             k = int(math.floor((self.time_to_expiry - t_mon) / dt + 1e-9))
             idx.add(max(1, min(self.num_time_steps, k)))
+        if len(_MON_CACHE) > 256:
+            _MON_CACHE.clear()
+        _MON_CACHE[key] = frozenset(idx)
         return idx
 
     def _ko_thresholds(self, s_nodes: Sequence[float], n_nodes: int,
@@ -405,7 +431,7 @@ class DiscreteBarrierFDMPricer:
         coeffs = operator_coefficients(sigma, self.carry_rate_nacc, self.div_yield_nacc,
                                        self.discount_rate_nacc, g.dx)
         n_nodes = g.n_space  # top node dropped on the first step (:449, :543)
-        v0 = self._payoff(g.s_nodes)[:n_nodes]
+        v0 = self._payoff(g.s_arr)[:n_nodes]
         lower, upper = self._boundaries(g.s_nodes)
         solve = Solve(it=False, n_time=n_steps, n_ranna=min(self.rannacher_steps, n_steps),
                       dt=dt, coeffs=coeffs, v_init=v0, lower=lower, upper=upper)
@@ -441,8 +467,7 @@ class DiscreteBarrierFDMPricer:
         """Non-uniform 3-point stencil at the interior node nearest spot (:949-978)."""
         s = self.s_nodes if s_nodes is None else s_nodes
         S0 = self.spot
-        sa = np.asarray(s[1:len(s) - 1])
-        idx = 1 + int(np.argmin(np.abs(sa - S0)))
+        idx = _nearest_interior(s, S0)  # 1 + argmin |s[1:-1] - S0|
         h1 = s[idx] - s[idx - 1]
         h2 = s[idx + 1] - s[idx]
         Vm, V0, Vp = V[idx - 1], V[idx], V[idx + 1]

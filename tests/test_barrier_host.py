@@ -107,3 +107,21 @@ def test_price_many_equals_sequential():
     for p, c in zip(batch, GOLD["cases"]):
         assert p.price_log2() == c["price_log2"]
         assert p.greeks_log2() == c["greeks_log2"]
+
+
+def test_nearest_interior_matches_argmin():
+    import numpy as np
+    from finite_difference_amd.barrier import _nearest_interior
+    rng = np.random.default_rng(4)
+    for _ in range(300):
+        n = int(rng.integers(4, 60))
+        s = np.sort(rng.uniform(0, 10, n))
+        if rng.integers(2):  # exact ties between neighbours
+            s = np.round(s, 1)
+            s = np.unique(s)
+            if len(s) < 4:
+                continue
+        sl = s.tolist()
+        for x in list(rng.uniform(-1, 11, 20)) + sl + [(a + b) / 2 for a, b in zip(sl, sl[1:])]:
+            ref = 1 + int(np.argmin(np.abs(np.asarray(sl[1:len(sl) - 1]) - x)))
+            assert _nearest_interior(sl, float(x)) == ref, (sl, x)
