@@ -102,17 +102,21 @@ def build_barrier(B: int, n_space: int, n_time: int, seed: int):
     kinds = ["up-and-out", "down-and-out", "up-and-in", "down-and-in"]
     solves = []
     S0 = 229.74
+    calc = {}  # one pricer per option type, re-pointed per scenario (scenarios.run_rows_batched)
     for i in range(B):
         bt = kinds[i % 4]
-        p = scenarios.make_barrier_pricer(
-            S0, float(rng.uniform(150, 300)), float(rng.uniform(0.15, 0.45)), 0.073086, bt,
-            float(rng.uniform(1.02, 1.5) * S0) if "up" in bt else None,
-            float(rng.uniform(0.6, 0.98) * S0) if "down" in bt else None,
-            base["valuation"], base["maturity"], base["monitor_dates"],
-            opt_type=("call", "put")[(i // 4) % 2], num_space_nodes=n_space,
-            num_time_steps=n_time, grid_mode="explicit")
-        ko = p._map_KI_to_KO() or p.barrier_type
-        p.barrier_type = ko
+        K, sig = float(rng.uniform(150, 300)), float(rng.uniform(0.15, 0.45))
+        up = float(rng.uniform(1.02, 1.5) * S0) if "up" in bt else None
+        lo = float(rng.uniform(0.6, 0.98) * S0) if "down" in bt else None
+        opt = ("call", "put")[(i // 4) % 2]
+        p = calc.get(opt)
+        if p is None:
+            p = calc[opt] = scenarios.make_barrier_pricer(
+                S0, K, sig, 0.073086, bt, up, lo, base["valuation"], base["maturity"],
+                base["monitor_dates"], opt_type=opt, num_space_nodes=n_space,
+                num_time_steps=n_time, grid_mode="explicit")
+        p._reset_trade(S0, K, sig, bt, lo, up)
+        p.barrier_type = p._map_KI_to_KO() or p.barrier_type
         solves.append(p._make_solve(True, p.sigma)[0])
     grp = pack(solves, list(range(B)))
     grp.top_dropped = True  # n_nodes = N_s configured nodes (…pricer.py:449, :543)

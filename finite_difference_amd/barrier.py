@@ -226,6 +226,27 @@ class DiscreteBarrierFDMPricer:
         self._requested_space_nodes = int(num_space_nodes)
         self._pde_cache: Dict[tuple, Dict[str, float]] = {}
 
+    def _reset_trade(self, spot: float, strike: float, sigma: float, barrier_type: str,
+                     lower_barrier: Optional[float], upper_barrier: Optional[float]) -> None:
+        """Re-point this pricer at another trade that shares its dates, curves,
+        dividends and numerics: the constructor's trade-dependent lines only
+        (:84-171).  The batch runner keeps one pricer per curve instead of
+        building one object (and one curve copy) per scenario row."""
+        if any(x <= 0 for x in (spot, strike, sigma)):
+            raise ValueError("spot, strike, sigma must be positive.")
+        self.spot, self.strike, self.sigma = spot, strike, sigma
+        self.barrier_type = barrier_type
+        self.lower_barrier, self.upper_barrier = lower_barrier, upper_barrier
+        self.div_yield_nacc = self.dividend_yield_nacc()
+        self.pv_divs = self.pv_dividends()
+        self.forward_price = self.spot * math.exp((self.carry_rate_nacc - self.div_yield_nacc)
+                                                  * self.time_to_carry)
+        self.b = math.log(self.forward_price / self.spot) / self.time_to_carry
+        self.num_space_nodes = self._requested_space_nodes  # configure_grid overwrites it
+        self.s_nodes = []
+        self._S_min = self._S_max = 0.0
+        self._pde_cache = {}
+
     @property
     def time_grid(self) -> List[float]:
         """t_i = i T / N_t (:170); built on first use, since the march never

@@ -147,6 +147,68 @@ def run_rows(rows: List[dict], base_params: Dict[str, Any],
     return out
 
 
+def run_rows_batched(rows: List[dict], base_params: Dict[str, Any],
+                     engine: Optional[Engine] = None,
+                     dv_sigma: float = 0.0001) -> List[Dict[str, Any]]:
+    """run_rows with one pricer per curve instead of one per row.
+
+    Every row of a scenario file shares the dates, monitoring calendar, lags
+    and numerics; only spot, strike, vol, rate and the barrier differ.  One
+    pricer per distinct rate is re-pointed at each row
+    (DiscreteBarrierFDMPricer._reset_trade) and the same methods as the
+    per-row path build the solves, finish the Greeks and price the
+    knock-in legs, so the results are identical to run_rows (tested); all
+    rows' solves go into one engine.run."""
+    from .barrier import KI_TO_KO, price_many  # noqa: F401  (same KO mapping)
+    calcs: Dict[float, DiscreteBarrierFDMPricer] = {}
+
+    def pricer_for(row) -> DiscreteBarrierFDMPricer:
+        rate = row["rate"]
+        p = calcs.get(rate)
+        if p is None:
+            p = make_barrier_pricer(row["S0"], row["K"], row["sigma"], rate, row["barrier_type"],
+                                    _opt(row, "upper_barrier"), _opt(row, "lower_barrier"),
+                                    engine=engine, **base_params)
+            calcs[rate] = p
+        p._reset_trade(row["S0"], row["K"], row["sigma"], row["barrier_type"],
+                       _opt(row, "lower_barrier"), _opt(row, "upper_barrier"))
+        return p
+
+    plan, solves = [], []
+    for row in rows:
+        p = pricer_for(row)
+        bt = p.barrier_type.lower()
+        kbt = None
+        if bt in ("down-and-out", "up-and-out") and not p.already_hit:
+            kbt = bt
+        elif bt in ("down-and-in", "up-and-in") and not p.already_in:
+            kbt = KI_TO_KO[bt]
+        if kbt is None:
+            plan.append((row, None, None, None, 0))
+            continue
+        p.barrier_type = kbt
+        (sb, gb), (su, gu) = p.pde_solves(True, dv_sigma)
+        plan.append((row, kbt, gb, gu, len(solves)))
+        solves.extend([sb, su])
+    res = (engine if engine is not None else next(iter(calcs.values()))._engine()).run(solves) \
+        if solves else []
+    out = []
+    for row, kbt, gb, gu, i in plan:
+        p = pricer_for(row)
+        if kbt is not None:
+            keep = p.barrier_type
+            p.barrier_type = kbt
+            p._pde_cache[p._pde_key(True, dv_sigma)] = p._pde_finish(res[i], gb, res[i + 1], gu,
+                                                                     dv_sigma)
+            p.barrier_type = keep
+        out.append(_barrier_row(row["scenario_name"], row["S0"], row["K"], row["sigma"],
+                                row["rate"], row["barrier_type"], _opt(row, "upper_barrier"),
+                                _opt(row, "lower_barrier"), p, _opt(row, "FA_price"),
+                                _opt(row, "FA_delta"), _opt(row, "FA_gamma"),
+                                _opt(row, "FA_vega")))
+    return out
+
+
 def run_all_scenarios(config_csv_path: str, output_csv_path: Optional[str],
                       base_params: Dict[str, Any], engine: Optional[Engine] = None,
                       verbose: bool = True):
@@ -158,7 +220,7 @@ def run_all_scenarios(config_csv_path: str, output_csv_path: Optional[str],
     cfg = pd.read_csv(config_csv_path)
     rows = [dict(r) for _, r in cfg.iterrows()]
     mine = distributed.shard(rows)
-    res = run_rows(mine, base_params, engine)
+    res = run_rows_batched(mine, base_params, engine)
     res = distributed.gather_rows(res)
     if res is None:  # non-zero rank
         return None
