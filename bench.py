@@ -75,14 +75,18 @@ def build_american(B: int, n_space: int, n_time: int, seed: int):
     val, mat = dt.date(2025, 7, 28), dt.date(2025, 8, 28)
     curve = market.iso_curve(market.create_rate_df(math.exp(0.07053828272) - 1.0))
     solves = []
+    p = None  # one pricer, re-pointed per scenario (same dates and curve)
     for i in range(B):
         j = (i * 2654435761 + seed * 97) % B  # deterministic shuffle
         strike = 140.0 + 70.0 * (j % 64) / 63.0
         sigma = 0.18 + 0.30 * ((j // 64) % 64) / 63.0
-        p = AmericanFDMPricer(spot=176.39, strike=strike, valuation_date=val, maturity_date=mat,
-                              sigma=sigma, option_type="put", discount_curve=curve,
-                              forward_curve=curve, num_space_nodes=n_space,
-                              num_time_steps=n_time, rannacher_steps=2)
+        if p is None:
+            p = AmericanFDMPricer(spot=176.39, strike=strike, valuation_date=val,
+                                  maturity_date=mat, sigma=sigma, option_type="put",
+                                  discount_curve=curve, forward_curve=curve,
+                                  num_space_nodes=n_space, num_time_steps=n_time,
+                                  rannacher_steps=2)
+        p._reset_trade(176.39, strike, sigma)
         p._build_log_grid()
         solves.append(p._segment_solve(p._payoff_array(), 0.0, p.time_to_expiry, n_time, True))
     return pack(solves, list(range(B)))

@@ -142,6 +142,18 @@ class AmericanFDMPricer:
         self.engine = engine
         self._cache: Dict[tuple, Tuple[np.ndarray, dict]] = {}
 
+    def _reset_trade(self, spot: float, strike: float, sigma: float) -> None:
+        """Re-point this pricer at another trade with the same dates, curves,
+        dividends, option type and numerics (the constructor's trade lines,
+        fd_american_equity.py:159-175); cached grids are kept, keyed by trade."""
+        if spot <= 0.0 or strike <= 0.0 or sigma <= 0.0:
+            raise ValueError("spot, strike and sigma must be positive.")
+        self.spot, self.strike, self.sigma = float(spot), float(strike), float(sigma)
+        self.spot_grid_index = self.spot_snapped = None
+        self.strike_grid_index = self.strike_snapped = None
+        self.s_nodes, self.x_nodes = [], []
+        self._S_min = self._S_max = self._dx = 0.0
+
     # ------------------------------------------------------------------ dates
     def _infer_denominator(self, day_count: str) -> int:
         return market.year_denominator(day_count)
