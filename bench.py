@@ -410,6 +410,9 @@ def main():
             "roofline_fp64_valu": {"achieved": achieved_tf, "peak": FP64_VALU_PEAK_TFLOPS,
                                    "unit": "TFLOP/s", "frac": achieved_tf / FP64_VALU_PEAK_TFLOPS,
                                    "flops_per_node_step": fps},
+            "roofline_note": ("algorithmic bytes per node-step (SURVEY 8d) over the HBM peak; the "
+                              "march keeps V in VGPRs, so HBM moves only `traffic` bytes per "
+                              "launch and the binding roof is fp64 VALU issue (DESIGN.md 4)"),
             "kernel_ms_per_launch": kernel_ms,
             "kernel": {"name": f"fdcn_march<IT={int(is_it)}>", **plan, "k_cap": k_cap},
             "outputs_finite": finite,
