@@ -232,6 +232,22 @@ struct KoMask {
   int k0, k1;
 };
 
+// Each wave's workspace row ends in kKoRow double2 = 64 per-slot knock-out
+// masks.  For NPT >= 48 the NPT masks (2 NPT SGPRs) do not fit the scalar
+// file: the compiler spilled them to VGPR lanes and read each back with two
+// v_readlane per slot and monitor step.  Those variants store the masks
+// once (vector stores) and reload them per monitor step with s_load, which
+// costs no VALU issue.
+constexpr int kKoRow = 32;
+typedef unsigned KoMask16 __attribute__((ext_vector_type(16)));  // 8 masks, s_load_dwordx16
+__device__ __forceinline__ unsigned long long ko_pair(KoMask16 m, int j) {
+  return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];
+}
+template <int IT, int NPT>
+struct KoLoad {
+  static constexpr bool value = !IT && NPT >= 48;
+};
+
 // ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
@@ -244,7 +260,7 @@ struct KArgs {
   const int32_t* mon_step;
   const double* mon_rebate;
   double* v_out;
-  double* bnd;      // workspace: Dirichlet values [B][W][n_pad][2]
+  double* bnd;      // workspace: Dirichlet values [B][W][n_pad + kKoRow][2]
   double* zg;       // workspace: correction tables [B][2][lz][NPT+1] (ZG variants)
   int n_pad;        // n_time rounded up to a multiple of 64
 };
@@ -314,7 +330,8 @@ fdcn_march(KArgs A) {
   // theta-form rhs term (-A_L)(lo_m + c2 lo_{m-1}) / (-A_U)(hi_m + c2 hi_{m-1})
   // (see the IT rhs below); IT has no knock-out, so lo_{m-1} is simply the
   // previous step's value and the whole term is tabulated here.
-  double2* bnd = reinterpret_cast<double2*>(A.bnd) + ((size_t)scen * W + wave) * A.n_pad;
+  double2* bnd =
+      reinterpret_cast<double2*>(A.bnd) + ((size_t)scen * W + wave) * (A.n_pad + kKoRow);
   const int lof = uni_i(I[FDCN_I_LO_FORM]), hif = uni_i(I[FDCN_I_HI_FORM]);
   const double l0 = uni(P[FDCN_P_LO_C0]), l1 = uni(P[FDCN_P_LO_E0]), l2 = uni(P[FDCN_P_LO_C1]),
                l3 = uni(P[FDCN_P_LO_E1]);
@@ -712,6 +729,20 @@ fdcn_march(KArgs A) {
       if (rh >= 0 && rh < 64) { kmh.part = 1ull << rh; kmh.k0 = sh; kmh.k1 = NPT - 1; }
     }
   }
+  unsigned long long kom_addr = 0;  // this wave's mask row (KoLoad variants)
+  if constexpr (KoLoad<IT, NPT>::value) {
+    unsigned long long* kom = reinterpret_cast<unsigned long long*>(bnd + A.n_pad);
+    if (lane < NPT) {
+      const int k = lane;
+      kom[k] = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) | kmh.full |
+               ((k >= kmh.k0 && k <= kmh.k1) ? kmh.part : 0ull);
+    }
+    // the loop reads the row back with s_load from inline asm, which the
+    // compiler's wait-count tracking does not see: drain the stores here
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    kom_addr = (unsigned long long)kom;
+  }
+  (void)kom_addr;
   int mpos = uni_i(I[FDCN_I_MON_START]);
   const int mend = mpos + uni_i(I[FDCN_I_MON_COUNT]);
   // monitor entry mpos (step, rebate) and the next one, loaded a monitor
@@ -992,10 +1023,71 @@ fdcn_march(KArgs A) {
       const double reb = cur_reb;
       double rebv = reb;  // VGPR copy: v_cndmask takes the mask as its SGPR operand
       asm volatile("" : "+v"(rebv));
-      // The per-slot masks are loop-invariant and the compiler hoists them;
-      // at NPT = 64 they spill to VGPR lanes (two v_readlane per slot).
-      // Rebuilding them here on the scalar unit instead measured slower
-      // (config 5: 29.1 -> 34.8 ms per launch), so the hoisted form stays.
+      // NPT <= 40: the per-slot masks are loop-invariant, the compiler
+      // hoists them and they stay in SGPRs.  NPT >= 48 (KoLoad): they would
+      // spill to VGPR lanes (two v_readlane per slot), so they are reloaded
+      // from the workspace row with s_load_dwordx16 (config 5: 29.3 -> 27.7
+      // ms per launch).  Rebuilding them on the scalar unit measured slower
+      // still (34.8 ms): SALU issue is one instruction per wave per cycle.
+      if constexpr (KoLoad<IT, NPT>::value) {
+        // eight slots per block: the block's sixteen v_cndmask run while the
+        // next block's eight masks arrive (one s_load_dwordx16, waited for
+        // at the end of the block, so every asm output is valid on exit)
+        const unsigned rlo = (unsigned)__double_as_longlong(rebv);
+        const unsigned rhi = (unsigned)(__double_as_longlong(rebv) >> 32);
+        // (laundered so the compiler cannot hoist the eight block
+        // addresses out of the time loop and spill them)
+        unsigned long long ka = kom_addr;
+        asm volatile("" : "+s"(ka));
+        KoMask16 mcur;
+        asm volatile("s_load_dwordx16 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(mcur)
+                     : "s"(ka)
+                     : "memory");
+#pragma unroll
+        for (int g = 0; g < NPT / 8; ++g) {
+          unsigned lo[8], hi[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            lo[j] = (unsigned)__double_as_longlong(V[8 * g + j]);
+            hi[j] = (unsigned)(__double_as_longlong(V[8 * g + j]) >> 32);
+          }
+          KoMask16 mnxt;
+          const bool more = g + 1 < NPT / 8;
+#define FDCN_KO_CND(j)                                                   \
+  "v_cndmask_b32 %[l" #j "], %[l" #j "], %[rl], %[m" #j "]\n\t"          \
+  "v_cndmask_b32 %[h" #j "], %[h" #j "], %[rh], %[m" #j "]\n\t"
+#define FDCN_KO_OPS                                                                         \
+  [l0] "+v"(lo[0]), [h0] "+v"(hi[0]), [l1] "+v"(lo[1]), [h1] "+v"(hi[1]), [l2] "+v"(lo[2]), \
+      [h2] "+v"(hi[2]), [l3] "+v"(lo[3]), [h3] "+v"(hi[3]), [l4] "+v"(lo[4]),               \
+      [h4] "+v"(hi[4]), [l5] "+v"(lo[5]), [h5] "+v"(hi[5]), [l6] "+v"(lo[6]),               \
+      [h6] "+v"(hi[6]), [l7] "+v"(lo[7]), [h7] "+v"(hi[7])
+#define FDCN_KO_INS                                                                     \
+  [rl] "v"(rlo), [rh] "v"(rhi), [m0] "s"(ko_pair(mcur, 0)), [m1] "s"(ko_pair(mcur, 1)), \
+      [m2] "s"(ko_pair(mcur, 2)), [m3] "s"(ko_pair(mcur, 3)), [m4] "s"(ko_pair(mcur, 4)), \
+      [m5] "s"(ko_pair(mcur, 5)), [m6] "s"(ko_pair(mcur, 6)), [m7] "s"(ko_pair(mcur, 7))
+          if (more) {
+            asm volatile("s_load_dwordx16 %[mn], %[ga], 0\n\t" FDCN_KO_CND(0) FDCN_KO_CND(1)
+                             FDCN_KO_CND(2) FDCN_KO_CND(3) FDCN_KO_CND(4) FDCN_KO_CND(5)
+                                 FDCN_KO_CND(6) FDCN_KO_CND(7) "s_waitcnt lgkmcnt(0)"
+                         : FDCN_KO_OPS, [mn] "=&s"(mnxt)
+                         : FDCN_KO_INS, [ga] "s"(ka + 64ull * (g + 1))
+                         : "memory");
+          } else {
+            asm volatile(FDCN_KO_CND(0) FDCN_KO_CND(1) FDCN_KO_CND(2) FDCN_KO_CND(3)
+                             FDCN_KO_CND(4) FDCN_KO_CND(5) FDCN_KO_CND(6) FDCN_KO_CND(7)
+                         : FDCN_KO_OPS
+                         : FDCN_KO_INS);
+          }
+#undef FDCN_KO_CND
+#undef FDCN_KO_OPS
+#undef FDCN_KO_INS
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            V[8 * g + j] = __longlong_as_double(((long long)hi[j] << 32) | lo[j]);
+          if (more) mcur = mnxt;
+        }
+      } else {
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         const unsigned long long mk = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) |
@@ -1009,6 +1101,7 @@ fdcn_march(KArgs A) {
                      : "+v"(lo), "+v"(hi)
                      : "v"(rlo), "v"(rhi), "s"(mk));
         V[k] = __longlong_as_double(((long long)hi << 32) | lo);
+      }
       }
       if (0 <= ko_lo) V0 = reb;
       if (n_nodes - 1 >= ko_hi) VN = reb;
@@ -1208,9 +1301,10 @@ int lds_doubles(const Variant& v, int lz) { return v.lds_per_scen(lz) * v.spb; }
 int pad64(int n) { return ((n > 0 ? n : 1) + 63) / 64 * 64; }
 
 // workspace bytes per scenario: one (lo, hi) Dirichlet pair per step and
-// wave; ZG variants add the correction table [2][lz][NPT+1]
+// wave plus the knock-out mask row (kKoRow) of each wave;
+// ZG variants add the correction table [2][lz][NPT+1]
 size_t bnd_bytes_per_scen(const Variant& v, int n_time) {
-  return sizeof(double) * 2 * (size_t)pad64(n_time) * (size_t)v.w;
+  return sizeof(double) * 2 * (size_t)(pad64(n_time) + kKoRow) * (size_t)v.w;
 }
 size_t ws_bytes_per_scen(const Variant& v, int n_time, int lz) {
   return bnd_bytes_per_scen(v, n_time) +
