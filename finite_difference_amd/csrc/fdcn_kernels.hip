@@ -385,6 +385,14 @@ fdcn_march(KArgs A) {
   double FW[6], GW[6];
   double Fpre = 0.0, Gsuf = 0.0;
   double mlast = 0.0, glast = 0.0;  // phantom slot: pass-through multipliers
+  // Lane masks folded into multipliers (no v_cndmask in the step).
+  // Inactive lanes hold exact zeros in every vector, so their zero-carry
+  // values and scan results are zero by themselves; only the carry an
+  // inactive lane receives from the last active one must be dropped, which
+  // the first forward pass-2 multipliers (fm_act, fmM_act: 0 there) do.
+  // The phantom slot's pass-2 multiplier mlast2 (0 on short lanes) writes
+  // the phantom's zero rhs instead of the passed-through value.
+  double fm_act = 0.0, fmM_act = 0.0, mlast2 = 0.0;
   double mulLF = 0.0, mulLB = 0.0;  // products across the last sub-chain
   double fmM = 0.0, bmM = 0.0;      // products across a full sub-chain
   int nst_f = 6, nst_b = 6;         // scan stages that carry weight above 1e-18
@@ -416,10 +424,13 @@ fdcn_march(KArgs A) {
     if constexpr (W > 1) __syncthreads();  // previous readers of Ftot/Gtot are done
     mlast = shrt ? 1.0 : p.fm;
     glast = shrt ? 1.0 : p.bm;
+    mlast2 = shrt ? 0.0 : p.fm;
+    fm_act = active ? p.fm : 0.0;
     const double fM1 = pow_n<NPT>(p.fm, M - 1), bM1 = pow_n<NPT>(p.bm, M - 1);
     fmM = uni(fM1 * p.fm);
     bmM = uni(bM1 * p.bm);
     mulLF = shrt ? fM1 : fmM;
+    fmM_act = active ? fmM : 0.0;
     mulLB = shrt ? bM1 : bmM;
     const int len = shrt ? NPT - 1 : NPT;
     double f = active ? pow_n<NPT>(p.fm, len) : 0.0;
@@ -503,7 +514,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
     for (int j = 1; j < S; ++j) e = fma(j == S - 1 ? mulLF : fmM, e, a[j]);
     FDCN_STAMP(st_acc, st_prev, 2);
-    double b = active ? e : 0.0;
+    double b = e;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
@@ -520,21 +531,20 @@ fdcn_march(KArgs A) {
     }
     double cin = shfl_up1(b, 1);  // DPP bound_ctrl: lane 0 receives 0 (= cw for W = 1)
     if (W > 1 && lane == 0) cin = cw;
-    if (!active) cin = 0.0;
     FDCN_STAMP(st_acc, st_prev, 3);
     // forward pass 2: carries into every sub-chain, then S chains in parallel
     double c[S];
     c[0] = cin;
 #pragma unroll
-    for (int j = 1; j < S; ++j) c[j] = fma(fmM, c[j - 1], a[j - 1]);
+    for (int j = 1; j < S; ++j) c[j] = fma(j == 1 ? fmM_act : fmM, c[j - 1], a[j - 1]);
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       double w = c[j];
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const int k = j * M + i;
-        w = fma(k == NPT - 1 ? mlast : fm, w, In(k));
-        Wr(k) = (k == NPT - 1 && shrt) ? 0.0 : w;
+        w = fma(k == NPT - 1 ? mlast2 : (k == 0 ? fm_act : fm), w, In(k));
+        Wr(k) = w;
       }
     }
     FDCN_STAMP(st_acc, st_prev, 4);
@@ -555,7 +565,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) e = fma(bmM, e, a[j]);
     FDCN_STAMP(st_acc, st_prev, 5);
-    double cb = active ? e : 0.0;
+    double cb = e;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
@@ -572,7 +582,6 @@ fdcn_march(KArgs A) {
     }
     double cinb = shfl_dn1(cb, 1);  // lane 63 receives 0 (= cwb for W = 1)
     if (W > 1 && lane == 63) cinb = cwb;
-    if (!active) cinb = 0.0;
     FDCN_STAMP(st_acc, st_prev, 6);
     c[S - 1] = cinb;
 #pragma unroll
@@ -765,6 +774,10 @@ fdcn_march(KArgs A) {
   // phase for step 0 (ph currently holds the theta the last table was built for)
   double smc;
   int tab;
+  // -smc on the lanes that hold table rows, 0 elsewhere: g = smc_l y0 needs
+  // no lane select
+  const double sm_row = (t < lz) ? -1.0 : 0.0;
+  double smc_l;
   // this lane's row of the correction tables (lanes >= lz read row lz-1)
   const int zoff_r = (t < lz ? t : lz - 1) * (NPT + 1);
   const int zoff_c = zoff_r + lz * (NPT + 1);
@@ -777,6 +790,7 @@ fdcn_march(KArgs A) {
     smc = smc_c;
     tab = 1;
   }
+  smc_l = sm_row * smc;
 
   double2 bnd_cur = make_double2(0.0, 0.0);
   double2 bnd_nxt = bnd[lane];  // steps 0..63
@@ -796,6 +810,7 @@ fdcn_march(KArgs A) {
       ph = make_phase(0.5, dt, ca, cc, cbc);
       setup_scan(ph);
       smc = smc_c;
+      smc_l = sm_row * smc;
       tab = 1;
     }
     if ((m & 63) == 0) {  // Dirichlet values of the next 64 steps, one per lane
@@ -830,8 +845,8 @@ fdcn_march(KArgs A) {
       // writes T, and x = (r u)/(theta r) - c2 V afterwards.
       const double blo = ph.th * (ph.pl * fma(ph.c2, V0, lo_new));
       const double bhi = ph.th * (ph.pu * fma(ph.c2, VN, hi_new));
-      vb0 = (t == 0) ? V[0] + blo : V[0];
-      vb1 = (t == L_act - 1) ? V[NPT - 1] + bhi : (shrt ? 0.0 : V[NPT - 1]);
+      vb0 = fma(e_first, blo, V[0]);
+      vb1 = shrt ? 0.0 : fma(e_last, bhi, V[NPT - 1]);  // knock-out may have set a phantom
     } else {
     if constexpr (W > 1) __syncthreads();  // halos of the previous step
     // neighbours' edge values: shuffled at the end of the previous step (W=1)
@@ -917,7 +932,7 @@ fdcn_march(KArgs A) {
       } else {
         y0 = (lz > 64) ? bcast_first(Out(0)) : read_lane(Out(0), 0);
       }
-      g = (t < lz) ? -(smc * y0) : 0.0;
+      g = smc_l * y0;
       // lane-major rows, stride NPT+1: bank-spread, immediate offsets
       zoff = opaque(tab ? zoff_c : zoff_r);
     }
