@@ -129,6 +129,27 @@ __device__ __forceinline__ double shfl_dn1(double x, int d) {
   return __shfl_down(x, (unsigned)d, 64);
 }
 
+// Scan-stage shifts for the time loop.  Strides 1-2 as above; longer ones
+// by ds_bpermute from lane4 = 4*lane held in one VGPR: the source lane is
+// (lane -/+ d) mod 64 (ds_bpermute uses the address bits [7:2]), so lanes
+// without a true source read another lane's finite value, which their zero
+// scan weight drops.  (__shfl_up/_down recompute a clamped address with
+// five VALU instructions per stage and step.)
+__device__ __forceinline__ double bperm(double x, int addr) {
+  const unsigned long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)(b & 0xffffffffull));
+  const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double scan_up(double x, int d, int lane4) {
+  if (d <= 2) return shfl_up1(x, d);
+  return bperm(x, lane4 - 4 * d);
+}
+__device__ __forceinline__ double scan_dn(double x, int d, int lane4) {
+  if (d <= 2) return shfl_dn1(x, d);
+  return bperm(x, lane4 + 4 * d);
+}
+
 __device__ __forceinline__ double bnd_eval(int form, double c0, double e0, double c1, double e1,
                                            double tau) {
   if (form == 1) return c0 * exp(e0 * tau) * c1 * exp(e1 * tau);
@@ -296,6 +317,8 @@ fdcn_march(KArgs A) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
 
   const int lane = threadIdx.x & 63;
+  int lane4 = lane << 2;
+  asm volatile("" : "+v"(lane4));  // one VGPR, never rematerialised in the loop
   const int wave_blk = uni_i(threadIdx.x >> 6);
   const int scen_in_blk = (W == 1) ? wave_blk : 0;
   const int wave = (W == 1) ? 0 : wave_blk;  // wave index within the scenario
@@ -518,7 +541,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      if (j < nst_f) b = fma(FW[j], shfl_up1(b, d), b);
+      if (j < nst_f) b = fma(FW[j], scan_up(b, d, lane4), b);
     }
     double cw = 0.0;
     if constexpr (W > 1) {
@@ -569,7 +592,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      if (j < nst_b) cb = fma(GW[j], shfl_dn1(cb, d), cb);
+      if (j < nst_b) cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
     }
     double cwb = 0.0;
     if constexpr (W > 1) {
