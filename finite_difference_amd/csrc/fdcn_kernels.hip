@@ -1064,15 +1064,16 @@ fdcn_march(KArgs A) {
       // NPT <= 40: the per-slot masks are loop-invariant, the compiler
       // hoists them and they stay in SGPRs.  NPT >= 48 (KoLoad): they would
       // spill to VGPR lanes (two v_readlane per slot), so they are reloaded
-      // from the workspace row with s_load_dwordx16 (config 5: 29.3 -> 27.7
-      // ms per launch).  Rebuilding them on the scalar unit measured slower
-      // still (34.8 ms): SALU issue is one instruction per wave per cycle.
+      // from the workspace row with s_load_dwordx16 and applied as one
+      // exec-masked v_mov_b64 per slot (config 5: 29.3 -> 26.0 ms per
+      // launch).  Rebuilding the masks on the scalar unit from (full, part,
+      // k0, k1) measured slower still (34.8 ms): five SALU per slot.
       if constexpr (KoLoad<IT, NPT>::value) {
-        // eight slots per block: the block's sixteen v_cndmask run while the
-        // next block's eight masks arrive (one s_load_dwordx16, waited for
-        // at the end of the block, so every asm output is valid on exit)
-        const unsigned rlo = (unsigned)__double_as_longlong(rebv);
-        const unsigned rhi = (unsigned)(__double_as_longlong(rebv) >> 32);
+        // eight slots per block: each slot is one v_mov_b64 of the rebate
+        // under an exec mask set on the scalar unit (s_and_b64 with the
+        // saved exec), while the next block's eight masks arrive (one
+        // s_load_dwordx16, waited for at the end of the block, so every asm
+        // output is valid on exit; exec is restored inside the block)
         // (laundered so the compiler cannot hoist the eight block
         // addresses out of the time loop and spill them)
         unsigned long long ka = kom_addr;
@@ -1084,45 +1085,38 @@ fdcn_march(KArgs A) {
                      : "memory");
 #pragma unroll
         for (int g = 0; g < NPT / 8; ++g) {
-          unsigned lo[8], hi[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            lo[j] = (unsigned)__double_as_longlong(V[8 * g + j]);
-            hi[j] = (unsigned)(__double_as_longlong(V[8 * g + j]) >> 32);
-          }
           KoMask16 mnxt;
           const bool more = g + 1 < NPT / 8;
-#define FDCN_KO_CND(j)                                                   \
-  "v_cndmask_b32 %[l" #j "], %[l" #j "], %[rl], %[m" #j "]\n\t"          \
-  "v_cndmask_b32 %[h" #j "], %[h" #j "], %[rh], %[m" #j "]\n\t"
-#define FDCN_KO_OPS                                                                         \
-  [l0] "+v"(lo[0]), [h0] "+v"(hi[0]), [l1] "+v"(lo[1]), [h1] "+v"(hi[1]), [l2] "+v"(lo[2]), \
-      [h2] "+v"(hi[2]), [l3] "+v"(lo[3]), [h3] "+v"(hi[3]), [l4] "+v"(lo[4]),               \
-      [h4] "+v"(hi[4]), [l5] "+v"(lo[5]), [h5] "+v"(hi[5]), [l6] "+v"(lo[6]),               \
-      [h6] "+v"(hi[6]), [l7] "+v"(lo[7]), [h7] "+v"(hi[7])
+          unsigned long long sv;
+#define FDCN_KO_MOV(j) "s_and_b64 exec, %[m" #j "], %[sv]\n\tv_mov_b64 %[v" #j "], %[rb]\n\t"
+#define FDCN_KO_OPS                                                                  \
+  [v0] "+v"(V[8 * g]), [v1] "+v"(V[8 * g + 1]), [v2] "+v"(V[8 * g + 2]),             \
+      [v3] "+v"(V[8 * g + 3]), [v4] "+v"(V[8 * g + 4]), [v5] "+v"(V[8 * g + 5]),     \
+      [v6] "+v"(V[8 * g + 6]), [v7] "+v"(V[8 * g + 7]), [sv] "=&s"(sv)
 #define FDCN_KO_INS                                                                     \
-  [rl] "v"(rlo), [rh] "v"(rhi), [m0] "s"(ko_pair(mcur, 0)), [m1] "s"(ko_pair(mcur, 1)), \
+  [rb] "v"(rebv), [m0] "s"(ko_pair(mcur, 0)), [m1] "s"(ko_pair(mcur, 1)),                \
       [m2] "s"(ko_pair(mcur, 2)), [m3] "s"(ko_pair(mcur, 3)), [m4] "s"(ko_pair(mcur, 4)), \
       [m5] "s"(ko_pair(mcur, 5)), [m6] "s"(ko_pair(mcur, 6)), [m7] "s"(ko_pair(mcur, 7))
           if (more) {
-            asm volatile("s_load_dwordx16 %[mn], %[ga], 0\n\t" FDCN_KO_CND(0) FDCN_KO_CND(1)
-                             FDCN_KO_CND(2) FDCN_KO_CND(3) FDCN_KO_CND(4) FDCN_KO_CND(5)
-                                 FDCN_KO_CND(6) FDCN_KO_CND(7) "s_waitcnt lgkmcnt(0)"
+            asm volatile("s_mov_b64 %[sv], exec\n\ts_load_dwordx16 %[mn], %[ga], 0\n\t"
+                         FDCN_KO_MOV(0) FDCN_KO_MOV(1) FDCN_KO_MOV(2) FDCN_KO_MOV(3)
+                         FDCN_KO_MOV(4) FDCN_KO_MOV(5) FDCN_KO_MOV(6) FDCN_KO_MOV(7)
+                         "s_mov_b64 exec, %[sv]\n\ts_waitcnt lgkmcnt(0)"
                          : FDCN_KO_OPS, [mn] "=&s"(mnxt)
                          : FDCN_KO_INS, [ga] "s"(ka + 64ull * (g + 1))
-                         : "memory");
+                         : "memory", "scc");
           } else {
-            asm volatile(FDCN_KO_CND(0) FDCN_KO_CND(1) FDCN_KO_CND(2) FDCN_KO_CND(3)
-                             FDCN_KO_CND(4) FDCN_KO_CND(5) FDCN_KO_CND(6) FDCN_KO_CND(7)
+            asm volatile("s_mov_b64 %[sv], exec\n\t"
+                         FDCN_KO_MOV(0) FDCN_KO_MOV(1) FDCN_KO_MOV(2) FDCN_KO_MOV(3)
+                         FDCN_KO_MOV(4) FDCN_KO_MOV(5) FDCN_KO_MOV(6) FDCN_KO_MOV(7)
+                         "s_mov_b64 exec, %[sv]"
                          : FDCN_KO_OPS
-                         : FDCN_KO_INS);
+                         : FDCN_KO_INS
+                         : "scc");
           }
-#undef FDCN_KO_CND
+#undef FDCN_KO_MOV
 #undef FDCN_KO_OPS
 #undef FDCN_KO_INS
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            V[8 * g + j] = __longlong_as_double(((long long)hi[j] << 32) | lo[j]);
           if (more) mcur = mnxt;
         }
       } else {
