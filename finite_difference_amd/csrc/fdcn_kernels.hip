@@ -47,6 +47,7 @@
 
 #include <algorithm>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/fdcn.h"
@@ -269,6 +270,17 @@ struct KoLoad {
   static constexpr bool value = !IT && NPT >= 48;
 };
 
+// CN variants marched in the recovery form (W = 1, NPT > 40; see the step
+// forms in fdcn_march).  Their Rannacher steps keep the old V in a
+// workspace slice [64][NPT] per scenario (host: ws_bytes_per_scen).
+__host__ __device__ constexpr bool rec_form(int it, int w, int npt) {
+#ifdef FDCN_NO_REC  // A/B builds only
+  return false && it && w && npt;
+#else
+  return !it && w == 1 && npt > 40;
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
@@ -283,6 +295,7 @@ struct KArgs {
   double* v_out;
   double* bnd;      // workspace: Dirichlet values [B][W][n_pad + kKoRow][2]
   double* zg;       // workspace: correction tables [B][2][lz][NPT+1] (ZG variants)
+  double* vsave;    // workspace: old V of a Rannacher step [B][64][NPT] (rec_form variants)
   int n_pad;        // n_time rounded up to a multiple of 64
 };
 
@@ -423,14 +436,25 @@ fdcn_march(KArgs A) {
   // Step forms (see the time loop):
   //   IT            state (V, Q), pointwise rhs V + Q, solve in place on V
   //   CN, kSplit    state V, rhs V (+ boundary terms), solve into T
+  //   CN, kRec      state V, rhs V (+ boundary terms), solve in place; the
+  //                 last backward pass recovers the old V (W = 1, NPT > 40)
   //   CN, stencil   state V, 3-point rhs in place (shifted layout); the
-  //                 variants whose V + T would not fit the register budget
+  //                 multi-wave variants whose V + T would not fit the
+  //                 register budget
 #ifdef FDCN_NO_SPLIT  // A/B builds only (tools/ab_build.sh)
   constexpr bool kSplit = false;
 #else
   constexpr bool kSplit = !IT && (W == 16 ? NPT <= 16 : NPT <= 40);
 #endif
-  constexpr bool kNatural = IT || kSplit;  // solve input in the natural layout
+  // CN, recover (W = 1, NPT > 40): state V only, pointwise rhs V solved in
+  // place; the update x = s u - c2 V needs the old V, which the last
+  // backward pass recovers from the forward-pass values it is about to
+  // overwrite (V_k = w_k - fm w_{k-1}), so no second vector is live.
+  // Rannacher steps (c2 = 0) add the old V back from a workspace copy.
+  // Config 5 (NPT = 64): 26.0 -> 23.8 ms per launch against the stencil form.
+  constexpr bool kRec = rec_form(IT, W, NPT);
+  static_assert(!(kRec && kSplit), "one step form per variant");
+  constexpr bool kNatural = IT || kSplit || kRec;  // solve input in the natural layout
   double V[NPT];
   double X = 0.0;  // node 0 of the shifted RHS layout (stencil CN; see solve)
   // IT: the second state vector Q = V/theta - W, where W is the last
@@ -438,6 +462,14 @@ fdcn_march(KArgs A) {
   double QS[IT ? NPT : 1];
   double T[kSplit ? NPT : 1];  // kSplit: the solve's work vector
   double vb0 = 0.0, vb1 = 0.0;  // kSplit: rhs of the chunk's first/last node
+  // kRec: boundary terms added to the rhs this step (recovery subtracts
+  // them), the solution at the chunk's node 0 before the update, and the
+  // per-lane update scale (0 on the phantom slot of short lanes)
+  double rec_lo = 0.0, rec_hi = 0.0, y0c = 0.0, s_l = 0.0;
+  (void)rec_lo;
+  (void)rec_hi;
+  (void)y0c;
+  (void)s_l;
   (void)QS;
   (void)T;
   (void)vb0;
@@ -505,12 +537,12 @@ fdcn_march(KArgs A) {
   // passes work in place on Wr (V for IT, T for kSplit) and return r times
   // the solution there.
   auto In = [&](int k) -> double {
-    if constexpr (IT) return V[k];
+    if constexpr (IT || kRec) return V[k];
     else if constexpr (kSplit) return k == 0 ? vb0 : (k == NPT - 1 ? vb1 : V[k]);
     else return k == 0 ? X : V[k - 1];
   };
   auto Wr = [&](int k) -> double& {
-    if constexpr (IT) return V[k];
+    if constexpr (IT || kRec) return V[k];
     else if constexpr (kSplit) return T[k];
     else return k == 0 ? X : V[k - 1];
   };
@@ -519,7 +551,9 @@ fdcn_march(KArgs A) {
     if constexpr (kSplit) return T[k];
     else return V[k];
   };
-  auto solve = [&](const Phase& p) __attribute__((always_inline)) {
+  // fz: std::true_type fuses the kRec update into the last backward pass
+  auto solve = [&](const Phase& p, auto fz) __attribute__((always_inline)) {
+    constexpr bool kFuse = decltype(fz)::value;
     const double fm = p.fm, bm = p.bm;
     // forward pass 1: zero-carry end value of every sub-chain
     double a[S];
@@ -560,6 +594,10 @@ fdcn_march(KArgs A) {
     c[0] = cin;
 #pragma unroll
     for (int j = 1; j < S; ++j) c[j] = fma(j == 1 ? fmM_act : fmM, c[j - 1], a[j - 1]);
+    double cf[S];  // kFuse: the values each sub-chain's first FMA multiplied
+#pragma unroll
+    for (int j = 0; j < S; ++j) cf[j] = c[j];
+    (void)cf;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       double w = c[j];
@@ -609,7 +647,58 @@ fdcn_march(KArgs A) {
     c[S - 1] = cinb;
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) c[j] = fma(j + 1 == S - 1 ? mulLB : bmM, c[j + 1], a[j + 1]);
-    if constexpr (kNatural) {
+    if constexpr (kFuse) {
+      // backward pass 2 fused with the kRec update, per node (descending):
+      //   u   = mul_b u + w_k                      (chain value, in uc[j])
+      //   -V_k = mul_f w_{k-1} - w_k (+ the boundary term added to the rhs)
+      //   x_k = s u - V_k                          (over V[k])
+      // w_{k-1} is still in V[k-1] (processed later in this pass) or, at a
+      // sub-chain's first node, the value its forward FMA multiplied (cf).
+      double uc[S];
+#pragma unroll
+      for (int j = 0; j < S; ++j) uc[j] = c[j];
+      // Per node index i, the S sub-chains' three FMAs are issued stage by
+      // stage (S chain steps, S recoveries, S updates), so no FMA waits on
+      // the one issued just before it.
+#pragma unroll
+      for (int i = M - 1; i >= 0; --i) {
+        double tt[S];
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          const int k = j * M + i;
+          if (k == NPT - 1)
+            asm volatile("v_fma_f64 %0, %1, %0, %2" : "+v"(uc[j]) : "v"(glast), "v"(V[k]));
+          else
+            asm volatile("v_fma_f64 %0, %1, %0, %2" : "+v"(uc[j]) : "s"(bm), "v"(V[k]));
+        }
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          const int k = j * M + i;
+          const double wprev = (i == 0) ? cf[j] : V[k - 1];
+          if (k == NPT - 1) {
+            asm volatile("v_fma_f64 %0, %1, %2, -%3"
+                         : "=v"(tt[j]) : "v"(mlast2), "v"(wprev), "v"(V[k]));
+            tt[j] = fma(e_last, rec_hi, tt[j]);
+          } else if (k == 0) {
+            asm volatile("v_fma_f64 %0, %1, %2, -%3"
+                         : "=v"(tt[j]) : "v"(fm_act), "v"(wprev), "v"(V[k]));
+            tt[j] = fma(e_first, rec_lo, tt[j]);
+          } else {
+            asm volatile("v_fma_f64 %0, %1, %2, -%3"
+                         : "=v"(tt[j]) : "s"(fm), "v"(wprev), "v"(V[k]));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          const int k = j * M + i;
+          if (k == NPT - 1)
+            asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "v"(s_l), "v"(uc[j]), "v"(tt[j]));
+          else
+            asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "s"(p.s), "v"(uc[j]), "v"(tt[j]));
+        }
+      }
+      y0c = uc[0];
+    } else if constexpr (kNatural) {
       // backward pass 2 in place (natural layout): y_k = mul*y_{k+1} + w_k
       // over Wr(k); the S sub-chains round-robin, as below
 #pragma unroll
@@ -677,10 +766,12 @@ fdcn_march(KArgs A) {
     } else {
       Wr(0) = (t == 0) ? p.inv_r : 0.0;
     }
-    solve(p);
+    solve(p, std::false_type{});
     if (t < lz) {
+      // the phantom slot of a short lane holds a pass-through value: store 0
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) ztab[(tab * lz + t) * (NPT + 1) + k] = Out(k);
+      for (int k = 0; k < NPT; ++k)
+        ztab[(tab * lz + t) * (NPT + 1) + k] = (k == NPT - 1 && shrt) ? 0.0 : Out(k);
     }
     const double z0 = bcast_first(Out(0));
     return uni(p.kappa / (1.0 + p.kappa * z0));
@@ -764,10 +855,14 @@ fdcn_march(KArgs A) {
   unsigned long long kom_addr = 0;  // this wave's mask row (KoLoad variants)
   if constexpr (KoLoad<IT, NPT>::value) {
     unsigned long long* kom = reinterpret_cast<unsigned long long*>(bnd + A.n_pad);
+    // kRec keeps the phantom slot of short lanes at zero: never knock it out
+    const unsigned long long shrt_lanes = kRec ? (unsigned long long)__ballot(shrt) : 0ull;
     if (lane < NPT) {
       const int k = lane;
-      kom[k] = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) | kmh.full |
-               ((k >= kmh.k0 && k <= kmh.k1) ? kmh.part : 0ull);
+      unsigned long long mk = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) |
+                              kmh.full | ((k >= kmh.k0 && k <= kmh.k1) ? kmh.part : 0ull);
+      if (k == NPT - 1) mk &= ~shrt_lanes;
+      kom[k] = mk;
     }
     // the loop reads the row back with s_load from inline asm, which the
     // compiler's wait-count tracking does not see: drain the stores here
@@ -814,6 +909,7 @@ fdcn_march(KArgs A) {
     tab = 1;
   }
   smc_l = sm_row * smc;
+  s_l = shrt ? 0.0 : ph.s;
 
   double2 bnd_cur = make_double2(0.0, 0.0);
   double2 bnd_nxt = bnd[lane];  // steps 0..63
@@ -834,6 +930,7 @@ fdcn_march(KArgs A) {
       setup_scan(ph);
       smc = smc_c;
       smc_l = sm_row * smc;
+      s_l = shrt ? 0.0 : ph.s;
       tab = 1;
     }
     if ((m & 63) == 0) {  // Dirichlet values of the next 64 steps, one per lane
@@ -870,6 +967,21 @@ fdcn_march(KArgs A) {
       const double bhi = ph.th * (ph.pu * fma(ph.c2, VN, hi_new));
       vb0 = fma(e_first, blo, V[0]);
       vb1 = shrt ? 0.0 : fma(e_last, bhi, V[NPT - 1]);  // knock-out may have set a phantom
+    } else if constexpr (kRec) {
+      // the kSplit rhs, in place (the phantom slot is kept at zero by the
+      // update and by the knock-out masks)
+      if (m < A.n_ranna) {
+        // Rannacher step: the update below returns s u - V_old, the step
+        // needs s u (c2 = 0); keep V_old for the add-back (lane-major, so
+        // every slot is an immediate offset from one address)
+        double* sv = A.vsave + ((size_t)scen * 64 + lane) * NPT;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) sv[k] = V[k];
+      }
+      rec_lo = ph.th * (ph.pl * fma(ph.c2, V0, lo_new));
+      rec_hi = ph.th * (ph.pu * fma(ph.c2, VN, hi_new));
+      V[0] = fma(e_first, rec_lo, V[0]);
+      V[NPT - 1] = fma(e_last, rec_hi, V[NPT - 1]);
     } else {
     if constexpr (W > 1) __syncthreads();  // halos of the previous step
     // neighbours' edge values: shuffled at the end of the previous step (W=1)
@@ -937,7 +1049,29 @@ fdcn_march(KArgs A) {
 
     FDCN_STAMP(st_acc, st_prev, 1);
     // ---- 2. tridiagonal solve ---------------------------------------------
-    solve(ph);
+    if constexpr (kRec) {
+      // one fused solve for both phases (a second, plain solve for the
+      // Rannacher steps doubled the live ranges: 373 registers, one wave per
+      // SIMD, 47.8 ms per config-5 launch instead of 26)
+      solve(ph, std::true_type{});
+      static_assert(!kRec || NPT % 8 == 0, "recovery variants add back 8 slots per group");
+      if (m < A.n_ranna) {
+        // x = (s u - V_old) + V_old, eight slots per group so the loads do
+        // not all hoist into registers
+        const double* sv = A.vsave + ((size_t)scen * 64 + lane) * NPT;
+#pragma unroll
+        for (int k = 0; k < NPT; k += 8) {
+          double o[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = sv[k + i];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) V[k + i] += o[i];
+          asm volatile("" ::: "memory");
+        }
+      }
+    } else {
+      solve(ph, std::false_type{});
+    }
     FDCN_STAMP(st_acc, st_prev, 7);
     // Sherman-Morrison: x = y - (k y0 / (1 + k z0)) z over the first lz lanes
     // (lanes >= lz use g = 0 and read row lz-1, one broadcast address), fused
@@ -950,7 +1084,9 @@ fdcn_march(KArgs A) {
     int zoff = 0;
     if (do_sm) {
       double y0;
-      if constexpr (W == 1) {
+      if constexpr (kRec) {
+        y0 = read_lane(y0c, 0);
+      } else if constexpr (W == 1) {
         y0 = read_lane(Out(0), 0);
       } else {
         y0 = (lz > 64) ? bcast_first(Out(0)) : read_lane(Out(0), 0);
@@ -978,6 +1114,8 @@ fdcn_march(KArgs A) {
         return kPhiLds ? phit[poff + k * L]
                        : ((active && node <= n_int) ? pin[poff + k] : 0.0);
       };
+      const double sg = kRec ? ph.s * g : 0.0;
+      (void)sg;
       double zn[4], pn[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1012,6 +1150,10 @@ fdcn_march(KArgs A) {
               : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(T[k]),
                 "+v"(T[k + 1]), "+v"(T[k + 2]), "+v"(T[k + 3])
               : "v"(g), "v"(zk[0]), "v"(zk[1]), "v"(zk[2]), "v"(zk[3]), "s"(ph.s));
+        } else if constexpr (kRec) {
+          // V holds s u already (both phases): x = s u + (s g) z
+#pragma unroll
+          for (int i = 0; i < 4; ++i) V[k + i] = fma(sg, zk[i], V[k + i]);
         } else if constexpr (!IT) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) V[k + i] = fma(g, zk[i], V[k + i]);
@@ -1334,13 +1476,17 @@ int pad64(int n) { return ((n > 0 ? n : 1) + 63) / 64 * 64; }
 
 // workspace bytes per scenario: one (lo, hi) Dirichlet pair per step and
 // wave plus the knock-out mask row (kKoRow) of each wave;
-// ZG variants add the correction table [2][lz][NPT+1]
+// ZG variants add the correction table [2][lz][NPT+1], rec_form variants
+// the Rannacher save slice [64][NPT]
 size_t bnd_bytes_per_scen(const Variant& v, int n_time) {
   return sizeof(double) * 2 * (size_t)(pad64(n_time) + kKoRow) * (size_t)v.w;
 }
+size_t zg_bytes_per_scen(const Variant& v, int lz) {
+  return v.zg ? sizeof(double) * 2 * (size_t)lz * (size_t)(v.npt + 1) : 0;
+}
 size_t ws_bytes_per_scen(const Variant& v, int n_time, int lz) {
-  return bnd_bytes_per_scen(v, n_time) +
-         (v.zg ? sizeof(double) * 2 * (size_t)lz * (size_t)(v.npt + 1) : 0);
+  return bnd_bytes_per_scen(v, n_time) + zg_bytes_per_scen(v, lz) +
+         (rec_form(v.it, v.w, v.npt) ? sizeof(double) * 64 * (size_t)v.npt : 0);
 }
 
 double host_fm(double theta, const double* P) {
@@ -1399,6 +1545,7 @@ int launch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   }
   a.bnd = workspace;
   a.zg = workspace + bnd_bytes_per_scen(*v, n_time) / sizeof(double) * (size_t)B;
+  a.vsave = a.zg + zg_bytes_per_scen(*v, lz) / sizeof(double) * (size_t)B;
   if (lds > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute((const void*)v->fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));

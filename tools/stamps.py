@@ -24,7 +24,8 @@ def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "american"
     builder, ns, nt, it, _ = bench.WORKLOADS[wl]
     B = int(sys.argv[2]) if len(sys.argv) > 2 else bench.DEFAULT_BATCH[wl]
-    L = ctypes.CDLL(os.path.join(ROOT, "finite_difference_amd", "_lib", "libfdcn_stamps.so"))
+    L = ctypes.CDLL(os.environ.get("FDCN_STAMPS_LIB") or
+                    os.path.join(ROOT, "finite_difference_amd", "_lib", "libfdcn_stamps.so"))
     g = builder(B, ns, nt, seed=0)
     D, I = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
     out = np.empty_like(g.v_init)
