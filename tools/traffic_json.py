@@ -51,8 +51,12 @@ def expected(wl):
     rd += len(g.mon_step) * 12
     bnd = g.B * waves * n_pad * 16
     ko_row = g.B * waves * plan["npt"] * 8 if (not is_it and plan["npt"] >= 48) else 0
+    # recovery-form variants (CN, W = 1, NPT > 40): the old V of each
+    # Rannacher step is written and read back once (64 x NPT doubles per wave)
+    rec = (g.B * 64 * plan["npt"] * 8 * min(g.n_ranna, g.n_time)
+           if (not is_it and waves == 1 and plan["npt"] > 40) else 0)
     key = f"{label}_{ns}x{nt}_batch{B}"
-    return key, rd + bnd + ko_row, vec + bnd + ko_row, plan
+    return key, rd + bnd + ko_row + rec, vec + bnd + ko_row + rec, plan
 
 
 def main():
@@ -79,7 +83,8 @@ def main():
             "plan": {"waves": plan["waves"], "npt": plan["npt"]},
             "note": ("compulsory bytes: inputs and monitor entries read once, v_out written "
                      "once, Dirichlet table (16 B per padded step per wave) and, for NPT >= 48 "
-                     "knock-out variants, the mask row written and read once; the march "
+                     "knock-out variants, the mask row written and read once (plus, for the "
+                     "recovery-form variants, the old V of each Rannacher step); the march "
                      "itself moves no HBM bytes per step"),
             "source": (f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, "
                        f"python bench.py --workload {wl} --steps 2 --warmup 1 "
