@@ -81,12 +81,22 @@ def _norm_cdf(x: float) -> float:
 
 
 class _Grid:
-    __slots__ = ("n_space", "n_time", "S_min", "S_max", "dx", "s_nodes", "s_arr")
+    """One log grid.  ``s_arr`` holds the nodes as a float64 array; the
+    reference's list form ``s_nodes`` is built on first access only (the
+    batched paths search and index the array and never need it)."""
+    __slots__ = ("n_space", "n_time", "S_min", "S_max", "dx", "s_arr", "_s_list")
 
-    def __init__(self, n_space, n_time, S_min, S_max, dx, s_nodes, s_arr=None):
+    def __init__(self, n_space, n_time, S_min, S_max, dx, s_arr):
         self.n_space, self.n_time = n_space, n_time
-        self.S_min, self.S_max, self.dx, self.s_nodes = S_min, S_max, dx, s_nodes
-        self.s_arr = s_arr  # the same nodes as a float64 array
+        self.S_min, self.S_max, self.dx = S_min, S_max, dx
+        self.s_arr = s_arr
+        self._s_list = None
+
+    @property
+    def s_nodes(self) -> List[float]:
+        if self._s_list is None:
+            self._s_list = self.s_arr.tolist()
+        return self._s_list
 
 
 class DiscreteBarrierFDMPricer:
@@ -361,7 +371,7 @@ class DiscreteBarrierFDMPricer:
         dx = (x_max - x_min) / n
         # [math.exp(x_min + i * dx) for i in range(n + 1)] (:358), in libfdcn
         s_arr = capi.log_grid(x_min, dx, n)[1]
-        return _Grid(n, self.num_time_steps, self._S_min, self._S_max, dx, s_arr.tolist(), s_arr)
+        return _Grid(n, self.num_time_steps, self._S_min, self._S_max, dx, s_arr)
 
     def _build_log_grid(self) -> float:
         g = self._grid()
@@ -386,8 +396,8 @@ class DiscreteBarrierFDMPricer:
         """Dirichlet values of :372-393 (put lower value keeps the S_min factor)."""
         r, b, k = self.discount_rate_nacc, self.carry_rate_nacc, self.strike
         if self.option_type.lower() == "call":
-            return Boundary(), Boundary(FORM_SUM, s_nodes[-1], b - r, -k, -r)
-        return Boundary(FORM_PROD, k, -r, s_nodes[0], b - r), Boundary()
+            return Boundary(), Boundary(FORM_SUM, float(s_nodes[-1]), b - r, -k, -r)
+        return Boundary(FORM_PROD, k, -r, float(s_nodes[0]), b - r), Boundary()
 
     def _monitor_indices_tau(self, dt: float) -> set:
         key = (dt, self.time_to_expiry, self.num_time_steps, tuple(self.monitor_times))
@@ -411,11 +421,12 @@ class DiscreteBarrierFDMPricer:
         _apply_KO_projection (:413-440) over nodes 0..n_nodes-1."""
         ko_lo, ko_hi = -1, n_nodes
         lo, up = self.lower_barrier, self.upper_barrier
-        s = list(s_nodes[:n_nodes])
+        # the same ordered compares as bisect over the list (increasing nodes)
+        s = np.asarray(s_nodes[:n_nodes], dtype=np.float64)
         if barrier_type in ("down-and-out", "double-out") and lo is not None:
-            ko_lo = bisect.bisect_right(s, lo) - 1      # last j with s_j <= lo
+            ko_lo = int(np.searchsorted(s, lo, side="right")) - 1  # last j with s_j <= lo
         if barrier_type in ("up-and-out", "double-out") and up is not None:
-            ko_hi = bisect.bisect_left(s, up)           # first j with s_j >= up
+            ko_hi = int(np.searchsorted(s, up, side="left"))       # first j with s_j >= up
         return ko_lo, ko_hi
 
     def _apply_KO_projection(self, V: List[float], s_nodes: List[float], tau_left: float) -> None:
@@ -452,12 +463,12 @@ class DiscreteBarrierFDMPricer:
         coeffs = operator_coefficients(sigma, self.carry_rate_nacc, self.div_yield_nacc,
                                        self.discount_rate_nacc, g.dx)
         n_nodes = g.n_space  # top node dropped on the first step (:449, :543)
-        v0 = self._payoff(g.s_arr)[:n_nodes]
-        lower, upper = self._boundaries(g.s_nodes)
+        v0 = self._payoff(g.s_arr[:n_nodes])
+        lower, upper = self._boundaries(g.s_arr)
         solve = Solve(it=False, n_time=n_steps, n_ranna=min(self.rannacher_steps, n_steps),
                       dt=dt, coeffs=coeffs, v_init=v0, lower=lower, upper=upper)
         if apply_KO and self.barrier_type in KO_TYPES:
-            solve.ko_lo, solve.ko_hi = self._ko_thresholds(g.s_nodes, n_nodes,
+            solve.ko_lo, solve.ko_hi = self._ko_thresholds(g.s_arr, n_nodes,
                                                            self.barrier_type)
             steps = sorted(k for k in self._monitor_indices_tau(dt) if 1 <= k <= n_steps)
             solve.mon_steps = steps
@@ -495,7 +506,7 @@ class DiscreteBarrierFDMPricer:
         delta = (-h2 / (h1 * (h1 + h2)) * Vm + (h2 - h1) / (h1 * h2) * V0
                  + h1 / (h2 * (h1 + h2)) * Vp)
         gamma = 2.0 * (Vm / (h1 * (h1 + h2)) - V0 / (h1 * h2) + Vp / (h2 * (h1 + h2)))
-        return delta, gamma
+        return float(delta), float(gamma)
 
     def _map_KI_to_KO(self) -> Optional[str]:
         return KI_TO_KO.get(self.barrier_type)
@@ -557,9 +568,9 @@ class DiscreteBarrierFDMPricer:
 
     def _pde_finish(self, Vb: np.ndarray, gb: _Grid, Vu: np.ndarray, gu: _Grid,
                     dv_sigma: float) -> Dict[str, float]:
-        price_base = self._interp_price(Vb, gb.s_nodes)
-        delta, gamma = self._delta_gamma_from_grid(Vb, gb.s_nodes)
-        price_up = self._interp_price(Vu, gu.s_nodes)
+        price_base = self._interp_price(Vb, gb.s_arr)
+        delta, gamma = self._delta_gamma_from_grid(Vb, gb.s_arr)
+        price_up = self._interp_price(Vu, gu.s_arr)
         vega = (price_up - price_base) / (dv_sigma * 100)
         theta = -(0.5 * self.sigma * self.sigma * self.spot * self.spot * gamma
                   + (self.carry_rate_nacc - self.div_yield_nacc) * self.spot * delta
