@@ -1,0 +1,96 @@
+"""GPU properties at the BASELINE grid sizes (size-independent checks).
+
+The oracle comparisons in test_gpu_kernels.py / test_gpu_pricers.py run at
+sizes the CPU oracle finishes in seconds (plus one full config-2 and config-5
+solve each).  These tests check properties that hold at any size, on the
+full grids of configs 2, 3 and 5 and through the variants the bench launches:
+
+* Ikonen-Toivanen (fd_american_equity.py:704-717): every interior node of the
+  result satisfies V >= payoff exactly (the update ends in max(phi, .)).
+* Knock-out projection (discrete_barrier_fdm_pricer.py:413-440, :545): when
+  the last step is a monitor step, every node at or beyond a threshold holds
+  the rebate exactly.
+* Linearity of the CN march (:475-543) with homogeneous Dirichlet values and
+  no projection: solve(v1 + 2 v2) = solve(v1) + 2 solve(v2) to rounding,
+  |diff| <= 1e-11 * max|solve|.
+* Empty batches return without a launch.
+"""
+import copy
+
+import numpy as np
+import pytest
+
+from finite_difference_amd import capi
+from finite_difference_amd.engine import Boundary, Engine
+from plan_factory import random_solve
+
+pytestmark = pytest.mark.gpu
+
+
+def test_it_config2_grid_respects_exercise_constraint():
+    rng = np.random.default_rng(2049)
+    solves = [random_solve(rng, 2049, 4096, 2, it=True) for _ in range(32)]
+    assert capi.plan(2049, True, B=4096)["npt"] == 32
+    out = Engine().run(solves)
+    for s, v in zip(solves, out):
+        assert np.all(np.isfinite(v))
+        inner = slice(1, len(v) - 1)
+        assert np.all(v[inner] >= s.payoff[inner]), "IT result below the payoff"
+
+
+@pytest.mark.parametrize("n_nodes,n_time", [(1024, 2000), (4096, 8192)], ids=["cfg3", "cfg5"])
+def test_ko_on_last_step_is_exact(n_nodes, n_time):
+    rng = np.random.default_rng(n_nodes)
+    solves = []
+    for i in range(12):
+        s = random_solve(rng, n_nodes, n_time, 2, it=False, ko=True)
+        s.ko_lo = n_nodes // 5 if i % 3 != 1 else -1
+        s.ko_hi = 4 * n_nodes // 5 if i % 3 != 0 else 1 << 30
+        steps = sorted(set(list(s.mon_steps) + [n_time]))
+        s.mon_steps = steps
+        s.mon_rebates = [1.5 if i % 2 else 0.0] * len(steps)
+        solves.append(s)
+    out = Engine().run(solves)
+    for s, v in zip(solves, out):
+        assert np.all(np.isfinite(v))
+        j = np.arange(len(v))
+        hit = (j <= s.ko_lo) | (j >= s.ko_hi)
+        assert hit.any()
+        assert np.all(v[hit] == s.mon_rebates[-1]), "knocked-out nodes differ from the rebate"
+        assert not np.all(v[~hit] == s.mon_rebates[-1])
+
+
+@pytest.mark.parametrize("variant", [None, "1,64"], ids=["latency", "rec_form"])
+def test_cn_config5_grid_is_linear(variant, monkeypatch):
+    if variant:
+        monkeypatch.setenv("FDCN_VARIANT", variant)
+    n_nodes, n_time = 4096, 8192
+    rng = np.random.default_rng(5)
+    base = random_solve(rng, n_nodes, n_time, 2, it=False, ko=False)
+    base.lower, base.upper = Boundary(), Boundary()
+    x = np.linspace(0.0, 1.0, n_nodes)
+    v1 = base.v_init.copy()
+    v1[0] = v1[-1] = 0.0
+    v2 = np.exp(-((x - 0.4) / 0.05) ** 2)
+    v2[0] = v2[-1] = 0.0
+    solves = []
+    for v in (v1, v2, v1 + 2.0 * v2):
+        s = copy.copy(base)
+        s.v_init = v
+        solves.append(s)
+    r1, r2, r12 = Engine().run(solves)
+    scale = max(1.0, float(np.max(np.abs(r12))))
+    err = float(np.max(np.abs(r12 - (r1 + 2.0 * r2)))) / scale
+    print(f"[linearity {variant or 'default'}] rel_err={err:.3e}")
+    assert err <= 1e-11
+    assert float(np.max(np.abs(r2))) > 1e-6  # the march did not zero the bump
+
+
+def test_empty_batch():
+    assert Engine().run([]) == []
+    out = capi.cn_batch(64, 10, 2, np.zeros((0, capi.NPARAM)), np.zeros((0, capi.NIPARAM)),
+                        np.zeros((0, 64)), [], [])
+    assert out.shape == (0, 64)
+    out = capi.it_batch(64, 10, 2, np.zeros((0, capi.NPARAM)), np.zeros((0, capi.NIPARAM)),
+                        np.zeros((0, 64)), np.zeros((0, 64)))
+    assert out.shape == (0, 64)
