@@ -317,6 +317,23 @@ __host__ __device__ inline int lds_doubles_per_scen(int lz) {
          (W > 1 ? Xch<W>::kSize : 0);
 }
 
+// Issue priority of the carry scans.  Between the two sweeps of a step a wave
+// runs a short dependent chain (sub-chain joins, the DPP scan, the carries);
+// raised priority lets it win the issue arbitration against the other wave
+// of its SIMD, which is streaming independent FMAs and fills the gaps.
+// Measured (tools/gpu_ab_n.sh, two calls): config 2 12.44 -> 12.22 ms, config 3
+// 6.66 -> 6.46 ms, config 5 unchanged; raising it also over the
+// Sherman-Morrison broadcast lost that again.  -DFDCN_PRIO=0 disables it.
+#ifndef FDCN_PRIO
+#define FDCN_PRIO 3
+#endif
+#if FDCN_PRIO > 0
+#define FDCN_PRIO_HI() __builtin_amdgcn_s_setprio(FDCN_PRIO)
+#define FDCN_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#else
+#define FDCN_PRIO_HI()
+#define FDCN_PRIO_LO()
+#endif
 #ifdef FDCN_WAVES_PER_EU  // A/B builds only: occupancy target for the W=1 variants
 #define FDCN_OCC_ATTR __attribute__((amdgpu_waves_per_eu(W == 1 ? FDCN_WAVES_PER_EU : 1)))
 #else
@@ -567,6 +584,7 @@ fdcn_march(KArgs A) {
       }
       a[j] = w;
     }
+    FDCN_PRIO_HI();
     double e = a[0];
 #pragma unroll
     for (int j = 1; j < S; ++j) e = fma(j == S - 1 ? mulLF : fmM, e, a[j]);
@@ -594,6 +612,7 @@ fdcn_march(KArgs A) {
     c[0] = cin;
 #pragma unroll
     for (int j = 1; j < S; ++j) c[j] = fma(j == 1 ? fmM_act : fmM, c[j - 1], a[j - 1]);
+    FDCN_PRIO_LO();
     double cf[S];  // kFuse: the values each sub-chain's first FMA multiplied
 #pragma unroll
     for (int j = 0; j < S; ++j) cf[j] = c[j];
@@ -622,6 +641,7 @@ fdcn_march(KArgs A) {
     }
     // zero-carry start value of the chunk: E_j = a[j] + prod(sub-chain j) E_{j+1};
     // sub-chains j <= S-2 never hold the phantom slot, so the product is bm^M
+    FDCN_PRIO_HI();
     e = a[S - 1];
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) e = fma(bmM, e, a[j]);
@@ -647,6 +667,7 @@ fdcn_march(KArgs A) {
     c[S - 1] = cinb;
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) c[j] = fma(j + 1 == S - 1 ? mulLB : bmM, c[j + 1], a[j + 1]);
+    FDCN_PRIO_LO();
     if constexpr (kFuse) {
       // backward pass 2 fused with the kRec update, per node (descending):
       //   u   = mul_b u + w_k                      (chain value, in uc[j])
