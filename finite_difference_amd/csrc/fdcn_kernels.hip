@@ -891,6 +891,14 @@ fdcn_march(KArgs A) {
     kom_addr = (unsigned long long)kom;
   }
   (void)kom_addr;
+  // every lane that holds a Sherman-Morrison table row is fully inside the
+  // lower knock-out region (sm_skip below)
+  bool sm_covered = false;
+  if constexpr (kRec) {
+    const unsigned long long lzm = lz >= 64 ? ~0ull : ((1ull << lz) - 1ull);
+    sm_covered = (kml.full & lzm) == lzm;
+  }
+  (void)sm_covered;
   int mpos = uni_i(I[FDCN_I_MON_START]);
   const int mend = mpos + uni_i(I[FDCN_I_MON_COUNT]);
   // monitor entry mpos (step, rebate) and the next one, loaded a monitor
@@ -1128,7 +1136,11 @@ fdcn_march(KArgs A) {
     // ---- 3. early exercise / boundaries / knock-out ------------------------
     const double cq = (m + 1 < A.n_ranna) ? 1.0 : 2.0;  // 1/theta of the next step (IT)
     (void)cq;
-    {
+    // kRec: the correction only changes nodes of lanes < lz; on a knock-out
+    // step whose lower side removes all of them the projection overwrites it
+    // with the rebate, so it is skipped (config 5 knocks out on every step)
+    const bool sm_skip = kRec && sm_covered && (m + 1 == next_mon);
+    if (!sm_skip) {
       const int poff = opaque(kPhiLds ? t : s_t + 1);
       auto phi_at = [&](int k) -> double {
         const int node = s_t + 1 + k;

@@ -138,3 +138,22 @@ def test_zero_steps_is_identity():
 
 def test_device_visible():
     assert capi.device_count() >= 1
+
+
+@pytest.mark.parametrize("ko_lo", [-1, 30, 1500], ids=["none", "inside_table", "covers_table"])
+def test_rec_form_every_step_knockout_vs_oracle(ko_lo, monkeypatch):
+    """Config-5 layout (W=1, NPT=64, recovery form) with a knock-out on every
+    step.  When the lower side covers the Sherman-Morrison lanes the kernel
+    skips the correction on those steps (the projection overwrites it)."""
+    monkeypatch.setenv("FDCN_VARIANT", "1,64")
+    n_nodes, n_time = 4096, 96
+    rng = np.random.default_rng(4096 + ko_lo)
+    solves = []
+    for i in range(4):
+        s = random_solve(rng, n_nodes, n_time, 2, it=False, ko=False)
+        s.ko_lo, s.ko_hi = ko_lo, 3500 if i % 2 else 1 << 30
+        s.mon_steps = list(range(1, n_time + 1))
+        s.mon_rebates = [0.0 if i < 2 else 0.75] * n_time
+        solves.append(s)
+    assert capi.plan(n_nodes, False, B=4)["npt"] == 64
+    _compare(solves, f"rec every-step KO ko_lo={ko_lo}")
