@@ -317,13 +317,16 @@ __host__ __device__ inline int lds_doubles_per_scen(int lz) {
          (W > 1 ? Xch<W>::kSize : 0);
 }
 
-// Issue priority of the carry scans.  Between the two sweeps of a step a wave
-// runs a short dependent chain (sub-chain joins, the DPP scan, the carries);
-// raised priority lets it win the issue arbitration against the other wave
-// of its SIMD, which is streaming independent FMAs and fills the gaps.
-// Measured (tools/gpu_ab_n.sh, two calls): config 2 12.44 -> 12.22 ms, config 3
-// 6.66 -> 6.46 ms, config 5 unchanged; raising it also over the
-// Sherman-Morrison broadcast lost that again.  -DFDCN_PRIO=0 disables it.
+// Issue priority of the zero-carry passes and the carry scans.  Each sweep
+// is pass 1 (aggregates), a short dependent chain (sub-chain joins, the DPP
+// scan, the carries), then pass 2.  Raised priority over pass 1 + scan lets
+// a wave reach its carries first while the other wave of its SIMD streams
+// the independent FMAs of its own pass 2 / update and fills the gaps.
+// Measured (tools/gpu_ab_n.sh): scans only: config 2 12.44 -> 12.22 ms,
+// config 3 6.66 -> 6.46 ms, config 5 unchanged; pass 1 + scan (this) a
+// further -1.3 / -2.2 % on config 2 (two boxes), -0.6 % on config 5, config
+// 3 neutral; raising it over the Sherman-Morrison broadcast lost time.
+// -DFDCN_PRIO=0 disables it.
 #ifndef FDCN_PRIO
 #define FDCN_PRIO 3
 #endif
@@ -572,6 +575,7 @@ fdcn_march(KArgs A) {
   auto solve = [&](const Phase& p, auto fz) __attribute__((always_inline)) {
     constexpr bool kFuse = decltype(fz)::value;
     const double fm = p.fm, bm = p.bm;
+    FDCN_PRIO_HI();  // pass 1 + scan raised, pass 2 at the base priority
     // forward pass 1: zero-carry end value of every sub-chain
     double a[S];
 #pragma unroll
@@ -584,7 +588,6 @@ fdcn_march(KArgs A) {
       }
       a[j] = w;
     }
-    FDCN_PRIO_HI();
     double e = a[0];
 #pragma unroll
     for (int j = 1; j < S; ++j) e = fma(j == S - 1 ? mulLF : fmM, e, a[j]);
@@ -628,6 +631,7 @@ fdcn_march(KArgs A) {
       }
     }
     FDCN_STAMP(st_acc, st_prev, 4);
+    FDCN_PRIO_HI();
     // backward pass 1: zero-carry start value of every sub-chain
 #pragma unroll
     for (int j = 0; j < S; ++j) {
@@ -641,7 +645,6 @@ fdcn_march(KArgs A) {
     }
     // zero-carry start value of the chunk: E_j = a[j] + prod(sub-chain j) E_{j+1};
     // sub-chains j <= S-2 never hold the phantom slot, so the product is bm^M
-    FDCN_PRIO_HI();
     e = a[S - 1];
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) e = fma(bmM, e, a[j]);
