@@ -428,12 +428,20 @@ fdcn_march(KArgs A) {
   // Each lane's NPT-node chunk is split into S sub-chains of M nodes.  The
   // recurrences run the S sub-chains interleaved (independent FMA chains) and
   // join them with a short Horner step in fm^M / bm^M, so a wave keeps S
-  // fp64 FMAs in flight instead of one dependent chain.
+  // fp64 FMAs in flight instead of one dependent chain.  The joins and
+  // their carries cost 2(S-1) FMAs per sweep and lane.  With the priority
+  // scheme above, the throughput variants (W = 1, 2-3 waves per SIMD) hide
+  // the FMA latency with the other waves: one chain (S = 1) measured
+  // fastest up to 40 nodes per lane, two at 48-64 (tools/gpu_ab_n.sh: config
+  // 2 12.31 -> 12.08 ms, config 3 6.54 -> 6.21 ms, config 5 20.65 -> 19.69 ms
+  // against S = 4).  The multi-wave variants serve small batches, where one
+  // wave per SIMD needs the in-wave ILP: they keep 4.
 #ifdef FDCN_SUBCHAINS  // A/B builds only
   constexpr int S = (NPT % FDCN_SUBCHAINS == 0 && NPT >= 4 * FDCN_SUBCHAINS) ? FDCN_SUBCHAINS
                     : ((NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1));
 #else
-  constexpr int S = (NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1);
+  constexpr int S = (W == 1) ? (NPT >= 48 ? 2 : 1)
+                             : ((NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1));
 #endif
   constexpr int M = NPT / S;
 
