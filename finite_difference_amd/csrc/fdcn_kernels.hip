@@ -1145,6 +1145,10 @@ fdcn_march(KArgs A) {
     }
     FDCN_STAMP(st_acc, st_prev, 8);
     // ---- 3. early exercise / boundaries / knock-out ------------------------
+    // IT: the update and the next RHS at priority 1, between pass 1 + scan
+    // (3) and pass 2 (0): config 2 11.99 -> 11.74 ms; the CN forms lost 2 %
+    // with it (tools/gpu_ab_n.sh)
+    if constexpr (IT && FDCN_PRIO > 0) __builtin_amdgcn_s_setprio(1);
     const double cq = (m + 1 < A.n_ranna) ? 1.0 : 2.0;  // 1/theta of the next step (IT)
     (void)cq;
     // kRec: the correction only changes nodes of lanes < lz; on a knock-out
