@@ -1145,10 +1145,11 @@ fdcn_march(KArgs A) {
     }
     FDCN_STAMP(st_acc, st_prev, 8);
     // ---- 3. early exercise / boundaries / knock-out ------------------------
-    // IT: the update and the next RHS at priority 1, between pass 1 + scan
-    // (3) and pass 2 (0): config 2 11.99 -> 11.74 ms; the CN forms lost 2 %
+    // IT and kRec: the update / knock-out and the next RHS at priority 1,
+    // between pass 1 + scan (3) and pass 2 (0): config 2 11.99 -> 11.74 ms,
+    // config 5 19.73 -> 18.41 ms (3 instead of 1: 18.65); kSplit lost 2 %
     // with it (tools/gpu_ab_n.sh)
-    if constexpr (IT && FDCN_PRIO > 0) __builtin_amdgcn_s_setprio(1);
+    if constexpr ((IT || kRec) && FDCN_PRIO > 0) __builtin_amdgcn_s_setprio(1);
     const double cq = (m + 1 < A.n_ranna) ? 1.0 : 2.0;  // 1/theta of the next step (IT)
     (void)cq;
     // kRec: the correction only changes nodes of lanes < lz; on a knock-out
