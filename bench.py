@@ -16,28 +16,42 @@ Other workloads (--workload, same JSON line format):
            1024 x 2000 grid, daily KO monitoring (run_config_scenarios.py).
   double   configs[4]: double knock-out call of double _barrier.py:139-146 on a
            4096 x 8192 grid, projection every step; --batch B sweeps sigma and
-           the barriers (B=1 is the single-solve latency case).
+           the barriers.
   analytic SURVEY §8(f) row 4, not a BASELINE config: 2^20 Reiner-Rubinstein
            barrier contracts (barrier_engine.py) per launch, one GPU thread
            each; its own metric line (contracts/s).
+Single-trade latency (one trade end to end through the drop-in facade, host
+plan building, launches, copies and the Greeks epilogue included; their own
+metric line, ms per trade):
+  trade_cnlog     configs[0]: DiscreteBarrierCrankNicolsonLog.price() of the
+                  discrete_barrier_fdm_main_cn.py trade, 512 x 1000 (3 solves)
+  trade_american  configs[1]: AmericanFDMPricer price_log2() + greeks_log2()
+                  of the notebook trade, 2048 x 4096 (6 unique solves)
+  trade_double    configs[4]: FDDoubleBarrier.price(b, r, T), 4096 x 8192
 
 value = total node-steps (configured nodes x steps x B x ranks) / max-over-
-ranks wall time of the K timed launches.
+ranks wall time of the K timed launches (whole-job aggregate).
 
-Multi-GPU: one process per GPU (torch.distributed.run); each rank marches its
-own B scenarios (weak scaling, no collective in the data path).
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set)
+each process is one rank; `--gpus N` without WORLD_SIZE spawns the N ranks
+itself (torch.multiprocessing, spawn start method) before anything touches a
+GPU.  Each rank binds GPU LOCAL_RANK and marches its own B scenarios (weak
+scaling, no collective in the data path; the only RCCL calls are the timing
+barrier and the max over ranks).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-                       [--workload american|barrier|double]
+                       [--workload NAME] [--dry-run]
 """
 from __future__ import annotations
 
 import argparse
 import datetime as dt
+import hashlib
 import json
 import math
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
@@ -45,28 +59,42 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
-FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec sheet, FP64 vector
-# algorithmic bytes / flops per node-step
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table (spec)
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec sheet, FP64 vector (FMA = 2 flops)
+VALU_CLOCK_GHZ = 2.4          # peak engine clock: 1024 SIMDs x 1 wave64 fp64 op / 4 clk
+N_SIMD = 1024
+# algorithmic bytes / flops per node-step of the reference
+# algorithm (DESIGN.md §4 derives them from fd_american_equity.py:681-717 and
+# discrete_barrier_fdm_pricer.py:531-546: RHS 5 (+2 for dt*lambda), Thomas
+# with the factorisation hoisted 5, IT update 5)
 BYTES_PER_NODE_STEP = {True: 32, False: 16}   # IT: V and lambda in+out; CN: V in+out
-FLOPS_PER_NODE_STEP = {True: 17, False: 10}   # RHS 5 (+2 lambda) + Thomas 5 (+ IT 5)
+FLOPS_PER_NODE_STEP = {True: 17, False: 10}
 DEFAULT_BATCH = {"american": 4096, "barrier": 10000, "double": 2048, "analytic": 1 << 20}
+TRADE_WORKLOADS = ("trade_cnlog", "trade_american", "trade_double")
+KERNEL_SRC = os.path.join(ROOT, "finite_difference_amd", "csrc", "fdcn_kernels.hip")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=sorted(DEFAULT_BATCH), default="american")
+    ap.add_argument("--workload", choices=sorted(DEFAULT_BATCH) + list(TRADE_WORKLOADS),
+                    default="american")
     ap.add_argument("--batch", type=int, default=0, help="scenarios per GPU (0: workload default)")
     ap.add_argument("--n-space", type=int, default=0, help="0: workload default")
     ap.add_argument("--n-time", type=int, default=0, help="0: workload default")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="exercise the rank spawn / gloo / timing / gather plumbing without "
+                         "a GPU (no march; the line is marked dry_run and is not a measurement)")
+    return ap.parse_args(argv)
 
 
+# ---------------------------------------------------------------------------
+# workloads
+# ---------------------------------------------------------------------------
 def build_american(B: int, n_space: int, n_time: int, seed: int):
     """B American puts of the notebook trade over a strike x vol sweep."""
     from finite_difference_amd import market
@@ -153,12 +181,64 @@ WORKLOADS = {  # name -> (builder, n_space, n_time, IT?, config label)
 }
 
 
+def node_units(group) -> int:
+    """Configured asset nodes of one solve (SURVEY §8(d)): N_s for the
+    top-node-dropping barrier march (n_nodes = N_s), n_nodes - 1 otherwise."""
+    return group.n_nodes if getattr(group, "top_dropped", False) else group.n_nodes - 1
+
+
+# ---------------------------------------------------------------------------
+# counters measured by tools/pmc_*.sh for THIS kernel source
+# ---------------------------------------------------------------------------
+def kernel_src_sha() -> str:
+    with open(KERNEL_SRC, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_counters(workload: str):
+    """{hbm_bytes_per_launch, valu_insts_per_launch, ...} from
+    profiles/pmc_counters.json for this workload -- only if they were measured
+    on the current kernel source (sha of fdcn_kernels.hip); stale numbers are
+    dropped (null), never reported."""
+    path = os.path.join(ROOT, "profiles", "pmc_counters.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(workload)
+    except Exception:
+        return None
+    if not rec or rec.get("kernel_src_sha") != kernel_src_sha():
+        return None
+    return rec
+
+
+# ---------------------------------------------------------------------------
+# CPU baselines (rank 0, N = 1): the oracle restatements on the host cores
+# ---------------------------------------------------------------------------
+def _cpu_model() -> str:
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
+        return next((l.split(":", 1)[1].strip() for l in out.splitlines()
+                     if l.startswith("Model name")), "") or platform.processor()
+    except Exception:
+        return platform.processor()
+
+
 def cpu_baseline(group, seconds: float):
-    """C oracle (sequential Thomas + IT per scenario, OpenMP over scenarios)
-    timed on a bounded prefix of the same batch."""
-    from oracle import oracle
-    nthreads = oracle.max_threads()
-    nthreads = min(nthreads, int(os.environ.get("OMP_NUM_THREADS", nthreads)))
+    """Two variants of the reference algorithm, each on a
+    bounded sample of the same batch:
+      (i)  C oracle: sequential Thomas (+ IT / KO) per scenario, the
+           reference's loops, OpenMP over scenarios on the host cores the
+           process may use;
+      (ii) NumPy batched over scenarios: the same loops with every per-node
+           operation vectorised across scenarios (one core).
+    The line's value is the faster one; both are listed."""
+    import numpy as np
+    from oracle import batched_numpy, oracle
+    affinity = len(os.sched_getaffinity(0))
+    nthreads = min(oracle.max_threads(), affinity,
+                   int(os.environ.get("OMP_NUM_THREADS", affinity)))
+    model = _cpu_model()
+    # (i) C oracle over whole scenarios, doubling the sample until `seconds`
     done, t_total, m = 0, 0.0, nthreads
     while t_total < seconds and done < group.B:
         m = min(m, group.B - done)
@@ -175,49 +255,344 @@ def cpu_baseline(group, seconds: float):
         t_total += time.perf_counter() - t0
         done += m
         m *= 2
-    units = done * node_units(group) * group.n_time
-    model = ""
-    try:
-        out = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
-        model = next((l.split(":", 1)[1].strip() for l in out.splitlines()
-                      if l.startswith("Model name")), "")
-    except Exception:
-        pass
-    return {"value": units / t_total, "unit": "node-steps/s", "cores": nthreads,
+    c_rate = done * node_units(group) * group.n_time / t_total
+    c_var = {"value": c_rate, "unit": "node-steps/s", "cores": nthreads, "kind": "port",
+             "variant": "C oracle, per-scenario Thomas, OpenMP over scenarios",
+             "sample": f"{done} of the {group.B} scenarios, full {node_units(group)}x"
+                       f"{group.n_time} grid, {t_total:.1f} s"}
+    # (ii) NumPy batched over up to 4096 scenarios, a prefix of the time steps
+    nb = min(group.B, 4096)
+    kw = dict(payoff=group.payoff[:nb]) if group.it else dict(
+        mon_step=group.mon_step, mon_rebate=group.mon_rebate)
+    steps, t_np = 1, 0.0
+    while True:
+        t0 = time.perf_counter()
+        batched_numpy.march(group.it, group.n_nodes, group.n_time, group.n_ranna,
+                            group.params[:nb], group.iparams[:nb], group.v_init[:nb],
+                            max_steps=steps, **kw)
+        t_np = time.perf_counter() - t0
+        if t_np > seconds / 3 or steps >= group.n_time:
+            break
+        steps = min(group.n_time, steps * 4)
+    np_rate = nb * node_units(group) * steps / t_np
+    np_var = {"value": np_rate, "unit": "node-steps/s", "cores": 1, "kind": "port",
+              "variant": "NumPy, Thomas vectorised over scenarios",
+              "sample": f"{nb} scenarios x first {steps} of {group.n_time} steps, full "
+                        f"{node_units(group)}-node grid, {t_np:.1f} s"}
+    best = c_var if c_rate >= np_rate else np_var
+    return {"value": best["value"], "unit": "node-steps/s", "cores": best["cores"],
             "kind": "port",
-            "sample": f"{done} of the {group.B} scenarios, full {node_units(group)}x"
-                      f"{group.n_time} grid, C oracle ("
-                      + ("Thomas + IT as fd_american_equity.py:559-726" if group.it else
-                         "Thomas + KO as discrete_barrier_fdm_pricer.py:442-547")
-                      + f"), {nthreads} OpenMP threads, {t_total:.1f} s on "
-                      f"{model or platform.processor()}"}
+            "sample": best["sample"] + f"; {best['variant']} ("
+                      + ("fd_american_equity.py:559-726" if group.it else
+                         "discrete_barrier_fdm_pricer.py:442-547")
+                      + f") on {model}",
+            "affinity_cpus": affinity, "variants": [c_var, np_var]}
 
 
-def node_units(group) -> int:
-    """Configured asset nodes of one solve (SURVEY §8(d)): N_s for the
-    top-node-dropping barrier march (n_nodes = N_s), n_nodes - 1 otherwise."""
-    return group.n_nodes if getattr(group, "top_dropped", False) else group.n_nodes - 1
+# ---------------------------------------------------------------------------
+# ranks
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def load_traffic(workload: str):
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        rec = d.get(workload)
-        return None if rec is None else rec.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+def _rank_entry(local_rank: int, argv, port: int, world: int) -> None:
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    run_rank(parse(argv))
+
+
+def spawn_ranks(args, argv) -> int:
+    """`--gpus N` without a launcher: start N rank processes (spawn: fresh
+    interpreters; this parent never touches a GPU) and wait for them."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_entry, args=(argv, _free_port(), args.gpus), nprocs=args.gpus,
+                       join=True, start_method="spawn")
+    return 0
+
+
+def run_rank(args):
+    if args.workload == "analytic":
+        return bench_analytic(args)
+    if args.workload in TRADE_WORKLOADS:
+        return bench_trade(args)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.dry_run:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.dry_run:
+        return dry_run_rank(args, world, rank, local)
+    from finite_difference_amd import capi, distributed
+    bound = distributed.bind_device()  # GPU LOCAL_RANK for libfdcn and torch
+    if bound is None:
+        raise capi.FdcnError("no gfx950 device visible; the benchmark needs an MI355X")
+    dev = torch.device("cuda", local)
+    builder, ns0, nt0, is_it, label = WORKLOADS[args.workload]
+    B = args.batch or DEFAULT_BATCH[args.workload]
+    n_space, n_time = args.n_space or ns0, args.n_time or nt0
+    t_build = time.perf_counter()
+    g = builder(B, n_space, n_time, seed=rank)
+    t_build = time.perf_counter() - t_build
+    k_cap = capi.sm_extent(g.n_nodes, g.n_time, g.n_ranna, g.params)
+    plan = capi.plan(g.n_nodes, is_it, k_cap, n_time=g.n_time, B=g.B)
+
+    P = torch.from_numpy(g.params).to(dev)
+    I = torch.from_numpy(g.iparams).to(dev)
+    V0 = torch.from_numpy(g.v_init).to(dev)
+    out = torch.empty_like(V0)
+    ws_bytes = max(8, plan["ws_bytes_per_scen"] * g.B)
+    ws = torch.empty(ws_bytes // 8, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream()
+    if is_it:
+        F = torch.from_numpy(g.payoff).to(dev)
+
+        def step():
+            capi.it_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, P.data_ptr(), I.data_ptr(),
+                              V0.data_ptr(), F.data_ptr(), out.data_ptr(), k_cap,
+                              ws.data_ptr(), ws_bytes, stream.cuda_stream)
+    else:
+        MS = torch.from_numpy(g.mon_step if len(g.mon_step) else np.zeros(1, np.int32)).to(dev)
+        MR = torch.from_numpy(g.mon_rebate if len(g.mon_rebate) else np.zeros(1)).to(dev)
+
+        def step():
+            capi.cn_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, P.data_ptr(), I.data_ptr(),
+                              V0.data_ptr(), len(g.mon_step), MS.data_ptr(), MR.data_ptr(),
+                              out.data_ptr(), k_cap, ws.data_ptr(), ws_bytes,
+                              stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # HIP events on the launch stream (the kernel runs on torch's current stream)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    res = out.cpu().numpy()
+    finite = bool(np.all(np.isfinite(res)))
+    node_steps_launch = g.B * node_units(g) * g.n_time  # configured nodes x steps x solves
+    total = node_steps_launch * args.steps * world
+    value = total / elapsed
+    workload = f"{label}_{n_space}x{n_time}_batch{B}"
+    bps, fps = BYTES_PER_NODE_STEP[is_it], FLOPS_PER_NODE_STEP[is_it]
+    kernel_s = kernel_ms * 1e-3
+    achieved_tf = fps * node_steps_launch / kernel_s / 1e12
+    achieved_gbs = bps * node_steps_launch / kernel_s / 1e9
+    ctr = load_counters(workload)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(g, args.cpu_seconds)
+
+    if rank == 0:
+        config = {"workload": workload, "scenarios_per_gpu": g.B, "grid": [n_space, n_time],
+                  "parallelism": f"scenario-sharded x{world}"}
+        if is_it:
+            config.update(option="american put", exercise="ikonen-toivanen", rannacher_steps=2)
+        elif args.workload == "barrier":
+            config.update(option="discrete barrier (up/down out/in, call/put)",
+                          monitoring="daily", rannacher_steps=2, grid_mode="explicit")
+        else:
+            config.update(option="double knock-out call", monitoring="every step",
+                          rannacher_steps=2)
+        valu = None
+        if ctr and ctr.get("valu_insts_per_launch"):
+            insts = float(ctr["valu_insts_per_launch"])
+            valu = {"valu_insts_per_node_step": insts / node_steps_launch,
+                    "issue_frac": insts * 4 / (N_SIMD * VALU_CLOCK_GHZ * 1e9 * kernel_s),
+                    "note": "SQ_INSTS_VALU of this kernel source (profiles/pmc_counters.json) "
+                            "x 4 clk per wave64 fp64 op / (1024 SIMDs x 2.4 GHz x launch time)"}
+        line = {
+            "metric": "CN grid-node-steps/sec/GPU (2048x4096 grid); achieved HBM GB/s vs peak",
+            "value": value,
+            "unit": "node-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (" + {"american": "strike x vol sweep of the notebook American put",
+                                     "barrier": "strike/vol/barrier sweep of the config_scenarios trade",
+                                     "double": "vol/barrier sweep of the double _barrier.py trade"}[
+                args.workload] + ")",
+            "config": config,
+            # the binding roof: the march keeps V in VGPRs, so HBM never binds
+            # (DESIGN.md §4); fp64 FMA throughput does
+            "roofline": {"bound": "fp64_valu", "achieved": achieved_tf,
+                         "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved_tf / FP64_VALU_PEAK_TFLOPS,
+                         "traffic": ctr.get("hbm_bytes_per_launch") if ctr else None,
+                         "flops_per_node_step": fps},
+            "roofline_hbm_effective": {
+                "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "bytes_per_node_step": bps,
+                "note": "algorithmic bytes (SURVEY 8d) / kernel time: an effective rate; the "
+                        "measured HBM traffic is roofline.traffic bytes per launch"},
+            "valu_issue": valu,
+            "value_per_gpu": value / world,
+            "kernel_ms_per_launch": kernel_ms,
+            "kernel": {"name": f"fdcn_march<IT={int(is_it)}>", **plan, "k_cap": k_cap,
+                       "src_sha": kernel_src_sha()},
+            "outputs_finite": finite,
+            "host_build_s": t_build,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dry_run_rank(args, world: int, rank: int, local: int):
+    """The multi-rank plumbing without a GPU: spawn, process group, barrier,
+    max-over-ranks timing and a gather of every rank's identity."""
+    import torch
+    import torch.distributed as dist
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ranks = [{"rank": rank, "local_rank": local, "pid": os.getpid()}]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        box = [None] * world if rank == 0 else None
+        dist.gather_object(ranks[0], box, dst=0)
+        ranks = box
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (no march)", "value": None, "unit": None,
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed / max(1, args.steps) * 1e3, "dry_run": True,
+                          "ranks": ranks}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
+# single-trade latency through the drop-in facades
+# ---------------------------------------------------------------------------
+def bench_trade(args):
+    """One trade end to end per step: construct the facade, price (and for
+    the American trade the Greeks), read the result -- host plan building,
+    H2D, launches, D2H and the epilogue all inside the timed region."""
+    from finite_difference_amd import capi, distributed
+    if distributed.bind_device() is None:
+        raise capi.FdcnError("no gfx950 device visible; the benchmark needs an MI355X")
+    from finite_difference_amd import market
+    from finite_difference_amd.american import AmericanFDMPricer, prefetch_many
+    from finite_difference_amd.cn_log import DiscreteBarrierCrankNicolsonLog
+    from finite_difference_amd.fd_barrier import FDDoubleBarrier
+
+    if args.workload == "trade_cnlog":
+        N, M = args.n_space or 512, args.n_time or 1000
+        mon = [d / 365 for d in (7, 10, 15, 21, 25, 30, 31)]
+
+        def trade():
+            p = DiscreteBarrierCrankNicolsonLog(
+                S0=229.74, K=220.0, T=31 / 365, sigma=0.261319016, r_disc=0.070538822,
+                b_carry=0.070538822, option_type="call", barrier_type="up-and-out",
+                upper_barrier=270.0, rebate=0.0, monitor_times=mon, N_space=N, N_time=M)
+            return {"price": p.price()}
+        solves, node_steps = 3, 3 * N * M
+        cfg = {"workload": f"trade_cnlog_{N}x{M}", "config": "BASELINE configs[0]",
+               "facade": "DiscreteBarrierCrankNicolsonLog.price() (base, sigma +- 1e-3)"}
+    elif args.workload == "trade_american":
+        N, M = args.n_space or 2048, args.n_time or 4096
+        val, mat = dt.date(2025, 7, 28), dt.date(2025, 8, 28)
+        curve = market.iso_curve(market.create_rate_df(math.exp(0.07053828272) - 1.0))
+
+        def trade():
+            p = AmericanFDMPricer(spot=176.39, strike=170.0, valuation_date=val,
+                                  maturity_date=mat, sigma=0.296783211249, option_type="put",
+                                  discount_curve=curve, forward_curve=curve,
+                                  num_space_nodes=N, num_time_steps=M, rannacher_steps=2)
+            prefetch_many([p])
+            g = p.greeks_log2()
+            g["price_log2"] = p.price_log2()
+            return g
+        grids = {(0, M), (0, 2 * N), (0, 2 * M), (1, M), (-1, M), (2, M), (-2, M)}
+        solves = len(grids)
+        node_steps = sum(N * nt for _, nt in grids)
+        cfg = {"workload": f"trade_american_{N}x{M}", "config": "BASELINE configs[1]",
+               "facade": "AmericanFDMPricer price_log2() + greeks_log2() "
+                         f"({solves} unique grids, one launch per step count)"}
+    else:
+        N, M = args.n_space or 4096, args.n_time or 8192
+
+        def trade():
+            d = FDDoubleBarrier(20.786, 21.0, 19.0, 23.0, 0.10994120968, "c", "out",
+                                n_space=N, n_time=M)
+            return {"price": d.price(0.049493018, 0.0709454892, 49 / 365)}
+        solves, node_steps = 1, N * M
+        cfg = {"workload": f"trade_double_{N}x{M}", "config": "BASELINE configs[4]",
+               "facade": "FDDoubleBarrier.price(b, r, T), knock-out every step"}
+
+    for _ in range(args.warmup):
+        trade()
+    times = []
+    res = None
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        res = trade()
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    ms = sum(times) / len(times) * 1e3
+    cfg["solves_per_trade"] = solves
+    print(json.dumps({
+        "metric": "single-trade latency through the drop-in facade",
+        "value": ms, "unit": "ms/trade", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "ms_min": times[0] * 1e3,
+        "ms_median": times[len(times) // 2] * 1e3, "higher_is_better": False,
+        "scaling": "none", "vs_baseline": None, "dtype": "f64",
+        "data": "the reference's own trade parameters", "config": cfg,
+        "node_steps_per_s": node_steps / (ms * 1e-3), "result": res}), flush=True)
 
 
 def bench_analytic(args):
     """Closed-form barrier batch (fdcn_rr_barrier_batch_dev): contracts/s."""
     import numpy as np
     import torch
-    from finite_difference_amd import capi
-    from finite_difference_amd.analytic import BarrierEngine, _rr_encode
+    from finite_difference_amd import capi, distributed
+    from finite_difference_amd.analytic import BarrierEngine
     capi.require_device()
-    dev = torch.device("cuda", 0)
+    distributed.bind_device()
+    dev = torch.device("cuda", distributed.local_rank())
     B = args.batch or DEFAULT_BATCH["analytic"]
     rng = np.random.default_rng(20250728)
     s = rng.uniform(50, 150, B)
@@ -287,142 +662,19 @@ def bench_analytic(args):
         "cpu_baseline": cpu}), flush=True)
 
 
-def main():
-    args = parse()
-    if args.workload == "analytic":
-        return bench_analytic(args)
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.workload in TRADE_WORKLOADS or args.workload == "analytic":
+            raise SystemExit(f"--workload {args.workload} is a single-GPU measurement")
+        return spawn_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    from finite_difference_amd import capi
-    capi.require_device()
-    builder, ns0, nt0, is_it, label = WORKLOADS[args.workload]
-    B = args.batch or DEFAULT_BATCH[args.workload]
-    n_space, n_time = args.n_space or ns0, args.n_time or nt0
-    t_build = time.perf_counter()
-    g = builder(B, n_space, n_time, seed=rank)
-    t_build = time.perf_counter() - t_build
-    k_cap = capi.sm_extent(g.n_nodes, g.n_time, g.n_ranna, g.params)
-    plan = capi.plan(g.n_nodes, is_it, k_cap, n_time=g.n_time, B=g.B)
-
-    P = torch.from_numpy(g.params).to(dev)
-    I = torch.from_numpy(g.iparams).to(dev)
-    V0 = torch.from_numpy(g.v_init).to(dev)
-    out = torch.empty_like(V0)
-    ws = torch.empty(max(1, plan["ws_bytes_per_scen"] * g.B // 8), dtype=torch.float64,
-                     device=dev)
-    stream = torch.cuda.current_stream()
-    if is_it:
-        F = torch.from_numpy(g.payoff).to(dev)
-
-        def step():
-            capi.it_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, P.data_ptr(), I.data_ptr(),
-                              V0.data_ptr(), F.data_ptr(), out.data_ptr(), k_cap,
-                              ws.data_ptr(), stream.cuda_stream)
-    else:
-        MS = torch.from_numpy(g.mon_step if len(g.mon_step) else np.zeros(1, np.int32)).to(dev)
-        MR = torch.from_numpy(g.mon_rebate if len(g.mon_rebate) else np.zeros(1)).to(dev)
-
-        def step():
-            capi.cn_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, P.data_ptr(), I.data_ptr(),
-                              V0.data_ptr(), len(g.mon_step), MS.data_ptr(), MR.data_ptr(),
-                              out.data_ptr(), k_cap, ws.data_ptr(), stream.cuda_stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / max(1, args.steps)  # HIP events, kernel stream
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    res = out.cpu().numpy()
-    finite = bool(np.all(np.isfinite(res)))
-    node_steps_launch = g.B * node_units(g) * g.n_time  # configured nodes x steps x solves
-    total = node_steps_launch * args.steps * world
-    value = total / elapsed
-    workload = f"{label}_{n_space}x{n_time}_batch{B}"
-    bps, fps = BYTES_PER_NODE_STEP[is_it], FLOPS_PER_NODE_STEP[is_it]
-    achieved_gbs = bps * node_steps_launch / (kernel_ms * 1e-3) / 1e9
-    achieved_tf = fps * node_steps_launch / (kernel_ms * 1e-3) / 1e12
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(g, args.cpu_seconds)
-
-    if rank == 0:
-        config = {"workload": workload, "scenarios_per_gpu": g.B, "grid": [n_space, n_time],
-                  "parallelism": f"scenario-sharded x{world}"}
-        if is_it:
-            config.update(option="american put", exercise="ikonen-toivanen", rannacher_steps=2)
-        elif args.workload == "barrier":
-            config.update(option="discrete barrier (up/down out/in, call/put)",
-                          monitoring="daily", rannacher_steps=2, grid_mode="explicit")
-        else:
-            config.update(option="double knock-out call", monitoring="every step",
-                          rannacher_steps=2)
-        line = {
-            "metric": "CN grid-node-steps/sec/GPU (2048x4096 grid); achieved HBM GB/s vs peak",
-            "value": value,
-            "unit": "node-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (" + {"american": "strike x vol sweep of the notebook American put",
-                                     "barrier": "strike/vol/barrier sweep of the config_scenarios trade",
-                                     "double": "vol/barrier sweep of the double _barrier.py trade"}[
-                args.workload] + ")",
-            "config": config,
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
-                         "traffic": load_traffic(workload)},
-            "roofline_fp64_valu": {"achieved": achieved_tf, "peak": FP64_VALU_PEAK_TFLOPS,
-                                   "unit": "TFLOP/s", "frac": achieved_tf / FP64_VALU_PEAK_TFLOPS,
-                                   "flops_per_node_step": fps},
-            "roofline_note": ("algorithmic bytes per node-step (SURVEY 8d) over the HBM peak; the "
-                              "march keeps V in VGPRs, so HBM moves only `traffic` bytes per "
-                              "launch and the binding roof is fp64 VALU issue (DESIGN.md 4)"),
-            "kernel_ms_per_launch": kernel_ms,
-            "kernel": {"name": f"fdcn_march<IT={int(is_it)}>", **plan, "k_cap": k_cap},
-            "outputs_finite": finite,
-            "host_build_s": t_build,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if args.gpus > 1 and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
+              file=sys.stderr)
+    return run_rank(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -28,14 +28,14 @@ P_HI_C0, P_HI_E0, P_HI_C1, P_HI_E1 = 9, 10, 11, 12
 NPARAM = 13
 I_LO_FORM, I_HI_FORM, I_KO_LO, I_KO_HI, I_MON_START, I_MON_COUNT, I_TAU_MODE = range(7)
 NIPARAM = 7
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batch_dev",
             "fdcn_plan", "fdcn_sm_extent", "fdcn_log_grid", "fdcn_dividend_jump",
             "fdcn_rr_barrier_batch",
             "fdcn_rr_barrier_batch_dev", "fdcn_double_barrier_batch",
             "fdcn_double_barrier_batch_dev", "fdcn_last_error", "fdcn_device_count",
-            "fdcn_abi_version")
+            "fdcn_abi_version", "fdcn_select_device", "fdcn_current_device")
 RR_NPARAM, RR_NFLAG = 8, 5
 DB_NPARAM, DB_NFLAG = 8, 3
 
@@ -51,6 +51,27 @@ _PD = ctypes.POINTER(ctypes.c_double)
 _PI = ctypes.POINTER(ctypes.c_int32)
 _I = ctypes.c_int32
 _V = ctypes.c_void_p
+_I64 = ctypes.c_int64
+
+
+def _preload_hip_runtime() -> None:
+    """Load the HIP runtime PyTorch ships (torch/lib/libamdhip64.so) before
+    libfdcn, so a process that uses both -- device tensors for the _dev entry
+    points, torch.distributed over RCCL -- has ONE HIP runtime.  libfdcn's
+    dependency (soname libamdhip64.so.7) then binds to the copy already
+    loaded; loading libfdcn first would map /opt/rocm's copy and torch would
+    later add a second one (its NEEDED entry is the unversioned name).
+    torch is not imported; without it /opt/rocm's runtime is used."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except Exception:
+        return
+    if spec is None or not spec.origin:
+        return
+    path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 
 
 def lib() -> ctypes.CDLL:
@@ -62,6 +83,7 @@ def lib() -> ctypes.CDLL:
                 raise FdcnError(
                     f"{LIB_PATH} is missing: build it with `python -c 'import "
                     f"__graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+            _preload_hip_runtime()
             L = ctypes.CDLL(LIB_PATH)
             L.fdcn_cn_batch.restype = _I
             L.fdcn_cn_batch.argtypes = [_I, _I, _I, _I, _PD, _PI, _PD, _I, _PI, _PD, _PD]
@@ -69,9 +91,9 @@ def lib() -> ctypes.CDLL:
             L.fdcn_it_batch.argtypes = [_I, _I, _I, _I, _PD, _PI, _PD, _PD, _PD]
             L.fdcn_cn_batch_dev.restype = _I
             L.fdcn_cn_batch_dev.argtypes = [_I, _I, _I, _I, _V, _V, _V, _I, _V, _V, _V, _I, _V,
-                                            _V]
+                                            _I64, _V]
             L.fdcn_it_batch_dev.restype = _I
-            L.fdcn_it_batch_dev.argtypes = [_I, _I, _I, _I, _V, _V, _V, _V, _V, _I, _V, _V]
+            L.fdcn_it_batch_dev.argtypes = [_I, _I, _I, _I, _V, _V, _V, _V, _V, _I, _V, _I64, _V]
             L.fdcn_plan.restype = _I
             L.fdcn_plan.argtypes = [_I, _I, _I, _I, _I, _PI, _PI, _PI, _PI,
                                     ctypes.POINTER(ctypes.c_int64)]
@@ -95,6 +117,10 @@ def lib() -> ctypes.CDLL:
             L.fdcn_device_count.argtypes = []
             L.fdcn_abi_version.restype = ctypes.c_int
             L.fdcn_abi_version.argtypes = []
+            L.fdcn_select_device.restype = ctypes.c_int
+            L.fdcn_select_device.argtypes = [_I]
+            L.fdcn_current_device.restype = ctypes.c_int
+            L.fdcn_current_device.argtypes = []
             if L.fdcn_abi_version() != ABI_VERSION:
                 raise FdcnError("libfdcn.so ABI version mismatch; rebuild")
             _lib = L
@@ -116,6 +142,19 @@ def require_device() -> None:
         raise FdcnError("no gfx950 (MI355X) device visible; the CN engine has no CPU path")
 
 
+def select_device(ordinal: int) -> None:
+    """Make `ordinal` the calling thread's HIP device (one process per GPU:
+    the local rank).  The host-array entry points run there."""
+    _check(lib().fdcn_select_device(int(ordinal)))
+
+
+def current_device() -> int:
+    d = int(lib().fdcn_current_device())
+    if d < 0:
+        _check(d)
+    return d
+
+
 def _f64(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.float64)
 
@@ -124,8 +163,11 @@ def _i32(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.int32)
 
 
-def plan(n_nodes: int, it_mode: bool, k_cap: int = 0, n_time: int = 1, B: int = 1 << 20) -> dict:
-    """Launch geometry for B scenarios (the default B is a large batch)."""
+def plan(n_nodes: int, it_mode: bool, k_cap: int = 0, n_time: int = 1, *, B: int) -> dict:
+    """Launch geometry for a launch of B scenarios.  B is required: the kernel
+    variant -- and so ws_bytes_per_scen -- depends on it (small batches spread
+    a scenario over more waves), and a workspace sized for another B is
+    rejected by the _dev entry points."""
     w, npt, spb, lds = (ctypes.c_int32() for _ in range(4))
     ws = ctypes.c_int64()
     _check(lib().fdcn_plan(B, n_nodes, n_time, 1 if it_mode else 0, k_cap, ctypes.byref(w),
@@ -175,19 +217,19 @@ def it_batch(n_nodes: int, n_time: int, n_ranna: int, params, iparams, v_init,
 def cn_batch_dev(B: int, n_nodes: int, n_time: int, n_ranna: int, params_ptr: int,
                  iparams_ptr: int, v_init_ptr: int, n_mon: int, mon_step_ptr: int,
                  mon_rebate_ptr: int, v_out_ptr: int, k_cap: int, workspace_ptr: int,
-                 stream_ptr: int) -> None:
+                 workspace_bytes: int, stream_ptr: int) -> None:
     """Device-pointer launch (asynchronous on `stream_ptr`)."""
     _check(lib().fdcn_cn_batch_dev(B, n_nodes, n_time, n_ranna, params_ptr, iparams_ptr,
                                    v_init_ptr, n_mon, mon_step_ptr, mon_rebate_ptr, v_out_ptr,
-                                   k_cap, workspace_ptr, stream_ptr))
+                                   k_cap, workspace_ptr, workspace_bytes, stream_ptr))
 
 
 def it_batch_dev(B: int, n_nodes: int, n_time: int, n_ranna: int, params_ptr: int,
                  iparams_ptr: int, v_init_ptr: int, payoff_ptr: int, v_out_ptr: int,
-                 k_cap: int, workspace_ptr: int, stream_ptr: int) -> None:
+                 k_cap: int, workspace_ptr: int, workspace_bytes: int, stream_ptr: int) -> None:
     _check(lib().fdcn_it_batch_dev(B, n_nodes, n_time, n_ranna, params_ptr, iparams_ptr,
                                    v_init_ptr, payoff_ptr, v_out_ptr, k_cap, workspace_ptr,
-                                   stream_ptr))
+                                   workspace_bytes, stream_ptr))
 
 
 def log_grid(x_min: float, dx: float, n: int):

@@ -84,28 +84,6 @@ __device__ __forceinline__ int opaque(int i) {
   return i;
 }
 
-// Diagnostic build only (-DFDCN_STAMPS): per-phase cycle counters of the time
-// loop, summed over waves into fdcn_stamps[] (read by fdcn_debug_stamps).  A
-// stamp is s_memtime + lgkmcnt(0) fenced by sched_barriers; it forbids overlap
-// across phases, so read the SHARES, never the diagnostic build's run time.
-#ifdef FDCN_STAMPS
-constexpr int kNumStamps = 9;
-__device__ unsigned long long fdcn_stamps[kNumStamps + 1];
-#define FDCN_STAMP(acc, prev, i)                                                  \
-  do {                                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                           \
-    unsigned long long now_;                                                     \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now_)::"memory");  \
-    acc[i] += now_ - prev;                                                       \
-    prev = now_;                                                                 \
-    __builtin_amdgcn_sched_barrier(0);                                           \
-  } while (0)
-#else
-#define FDCN_STAMP(acc, prev, i) \
-  do {                           \
-  } while (0)
-#endif
-
 // Cross-lane moves.  Shifts by one lane use the GFX9 wavefront DPP shifts
 // (wave_shr:1 / wave_shl:1: two VALU moves, no LDS round trip), by two lanes
 // two of them; longer shifts go through ds_bpermute.  Lanes without a source
@@ -274,11 +252,7 @@ struct KoLoad {
 // forms in fdcn_march).  Their Rannacher steps keep the old V in a
 // workspace slice [64][NPT] per scenario (host: ws_bytes_per_scen).
 __host__ __device__ constexpr bool rec_form(int it, int w, int npt) {
-#ifdef FDCN_NO_REC  // A/B builds only
-  return false && it && w && npt;
-#else
   return !it && w == 1 && npt > 40;
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -326,24 +300,10 @@ __host__ __device__ inline int lds_doubles_per_scen(int lz) {
 // config 3 6.66 -> 6.46 ms, config 5 unchanged; pass 1 + scan (this) a
 // further -1.3 / -2.2 % on config 2 (two boxes), -0.6 % on config 5, config
 // 3 neutral; raising it over the Sherman-Morrison broadcast lost time.
-// -DFDCN_PRIO=0 disables it.
-#ifndef FDCN_PRIO
-#define FDCN_PRIO 3
-#endif
-#if FDCN_PRIO > 0
-#define FDCN_PRIO_HI() __builtin_amdgcn_s_setprio(FDCN_PRIO)
+#define FDCN_PRIO_HI() __builtin_amdgcn_s_setprio(3)
 #define FDCN_PRIO_LO() __builtin_amdgcn_s_setprio(0)
-#else
-#define FDCN_PRIO_HI()
-#define FDCN_PRIO_LO()
-#endif
-#ifdef FDCN_WAVES_PER_EU  // A/B builds only: occupancy target for the W=1 variants
-#define FDCN_OCC_ATTR __attribute__((amdgpu_waves_per_eu(W == 1 ? FDCN_WAVES_PER_EU : 1)))
-#else
-#define FDCN_OCC_ATTR
-#endif
 template <int IT, int W, int NPT, int ZG = 0>
-__global__ void __launch_bounds__(64 * W) FDCN_OCC_ATTR
+__global__ void __launch_bounds__(64 * W)
 fdcn_march(KArgs A) {
   constexpr int L = Geo<IT, W, NPT, ZG>::L;
   constexpr int SPB = Geo<IT, W, NPT, ZG>::SPB;
@@ -381,7 +341,9 @@ fdcn_march(KArgs A) {
   // Dirichlet values of every step, evaluated once up front (while few
   // registers are live) into this wave's workspace row: lane l owns steps
   // m = l (mod 64) and is the only lane that reads them back, so no
-  // synchronisation is needed.  tau_m = tau0 + (m+1) dt (…pricer.py:519).
+  // synchronisation is needed.  tau_m = tau0 + (m+1) dt (…pricer.py:519),
+  // or with FDCN_I_TAU_MODE = 1 the reference American loop's accumulated
+  // tau (tau = tau + dt per step, fd_american_equity.py:664-724).
   // IT: what the step needs is not the Dirichlet value itself but its
   // theta-form rhs term (-A_L)(lo_m + c2 lo_{m-1}) / (-A_U)(hi_m + c2 hi_{m-1})
   // (see the IT rhs below); IT has no knock-out, so lo_{m-1} is simply the
@@ -393,14 +355,35 @@ fdcn_march(KArgs A) {
                l3 = uni(P[FDCN_P_LO_E1]);
   const double h0 = uni(P[FDCN_P_HI_C0]), h1 = uni(P[FDCN_P_HI_E0]), h2 = uni(P[FDCN_P_HI_C1]),
                h3 = uni(P[FDCN_P_HI_E1]);
+  const int tau_mode = uni_i(I[FDCN_I_TAU_MODE]);
+  double tau_end = tau0 + (double)A.n_time * dt;  // tau after the last step
+  if (tau_mode == 1) {
+    // The accumulated sequence is inherently serial: every lane runs the
+    // same chain of adds (one per step, ~20 us for 4096 steps), and the
+    // owner lane of step m parks (tau_m, tau_{m-1}) in its workspace slot,
+    // which the tabulation below reads back before overwriting it.
+    double tc = tau0;
+    for (int m = 0; m < A.n_pad; ++m) {
+      const double tp = tc;
+      tc = tc + dt;
+      if (m + 1 == A.n_time) tau_end = tc;
+      if ((m & 63) == lane) bnd[m] = make_double2(tc, tp);
+    }
+    __threadfence_block();
+  }
   {
     const double* vb = A.v_init + (size_t)scen * n_nodes;
     const double v_lo0 = IT ? uni(vb[0]) : 0.0, v_hi0 = IT ? uni(vb[n_nodes - 1]) : 0.0;
     for (int m = lane; m < A.n_pad; m += 64) {
-      const double tau = tau0 + (double)(m + 1) * dt;
+      double tau = tau0 + (double)(m + 1) * dt, tp = tau0 + (double)m * dt;
+      if (tau_mode == 1) {
+        const double2 tt = bnd[m];
+        tau = tt.x;
+        tp = tt.y;
+      }
+      (void)tp;
       const double lo = bnd_eval(lof, l0, l1, l2, l3, tau), hi = bnd_eval(hif, h0, h1, h2, h3, tau);
       if constexpr (IT) {
-        const double tp = tau0 + (double)m * dt;
         const double lo_p = m == 0 ? v_lo0 : bnd_eval(lof, l0, l1, l2, l3, tp);
         const double hi_p = m == 0 ? v_hi0 : bnd_eval(hif, h0, h1, h2, h3, tp);
         const double th = m < A.n_ranna ? 1.0 : 0.5;
@@ -436,13 +419,8 @@ fdcn_march(KArgs A) {
   // 2 12.31 -> 12.08 ms, config 3 6.54 -> 6.21 ms, config 5 20.65 -> 19.69 ms
   // against S = 4).  The multi-wave variants serve small batches, where one
   // wave per SIMD needs the in-wave ILP: they keep 4.
-#ifdef FDCN_SUBCHAINS  // A/B builds only
-  constexpr int S = (NPT % FDCN_SUBCHAINS == 0 && NPT >= 4 * FDCN_SUBCHAINS) ? FDCN_SUBCHAINS
-                    : ((NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1));
-#else
   constexpr int S = (W == 1) ? (NPT >= 48 ? 2 : 1)
                              : ((NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1));
-#endif
   constexpr int M = NPT / S;
 
   // ---- per-theta constants: scan window products + SM table -------------
@@ -469,11 +447,7 @@ fdcn_march(KArgs A) {
   //   CN, stencil   state V, 3-point rhs in place (shifted layout); the
   //                 multi-wave variants whose V + T would not fit the
   //                 register budget
-#ifdef FDCN_NO_SPLIT  // A/B builds only (tools/ab_build.sh)
-  constexpr bool kSplit = false;
-#else
   constexpr bool kSplit = !IT && (W == 16 ? NPT <= 16 : NPT <= 40);
-#endif
   // CN, recover (W = 1, NPT > 40): state V only, pointwise rhs V solved in
   // place; the update x = s u - c2 V needs the old V, which the last
   // backward pass recovers from the forward-pass values it is about to
@@ -552,11 +526,6 @@ fdcn_march(KArgs A) {
     }
   };
 
-#ifdef FDCN_STAMPS
-  unsigned long long st_acc[kNumStamps] = {0};
-  unsigned long long st_prev = 0;
-  bool st_on = false;  // count only inside the time loop
-#endif
   // Forward + backward sweeps.  Stencil CN input: rhs/r in the SHIFTED
   // layout left by the in-place RHS (node 0 in X, node k >= 1 in V[k-1]);
   // the last backward pass writes node k into V[k] while reading node k's
@@ -599,7 +568,6 @@ fdcn_march(KArgs A) {
     double e = a[0];
 #pragma unroll
     for (int j = 1; j < S; ++j) e = fma(j == S - 1 ? mulLF : fmM, e, a[j]);
-    FDCN_STAMP(st_acc, st_prev, 2);
     double b = e;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -617,7 +585,6 @@ fdcn_march(KArgs A) {
     }
     double cin = shfl_up1(b, 1);  // DPP bound_ctrl: lane 0 receives 0 (= cw for W = 1)
     if (W > 1 && lane == 0) cin = cw;
-    FDCN_STAMP(st_acc, st_prev, 3);
     // forward pass 2: carries into every sub-chain, then S chains in parallel
     double c[S];
     c[0] = cin;
@@ -638,7 +605,6 @@ fdcn_march(KArgs A) {
         Wr(k) = w;
       }
     }
-    FDCN_STAMP(st_acc, st_prev, 4);
     FDCN_PRIO_HI();
     // backward pass 1: zero-carry start value of every sub-chain
 #pragma unroll
@@ -656,7 +622,6 @@ fdcn_march(KArgs A) {
     e = a[S - 1];
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) e = fma(bmM, e, a[j]);
-    FDCN_STAMP(st_acc, st_prev, 5);
     double cb = e;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -674,7 +639,6 @@ fdcn_march(KArgs A) {
     }
     double cinb = shfl_dn1(cb, 1);  // lane 63 receives 0 (= cwb for W = 1)
     if (W > 1 && lane == 63) cinb = cwb;
-    FDCN_STAMP(st_acc, st_prev, 6);
     c[S - 1] = cinb;
 #pragma unroll
     for (int j = S - 2; j >= 0; --j) c[j] = fma(j + 1 == S - 1 ? mulLB : bmM, c[j + 1], a[j + 1]);
@@ -912,6 +876,9 @@ fdcn_march(KArgs A) {
   (void)sm_covered;
   int mpos = uni_i(I[FDCN_I_MON_START]);
   const int mend = mpos + uni_i(I[FDCN_I_MON_COUNT]);
+  // entries < 1 never match a step: skip them (the oracle's `while` does)
+  if (!IT)
+    while (mpos < mend && uni_i(A.mon_step[mpos]) < 1) ++mpos;
   // monitor entry mpos (step, rebate) and the next one, loaded a monitor
   // step ahead of their use so the scalar-load latency is off the step
   int next_mon = 0x7fffffff, pf_mon = 0x7fffffff;
@@ -958,12 +925,6 @@ fdcn_march(KArgs A) {
     halo_l = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
     halo_r = shfl_dn1(V[0], 1);
   }
-#ifdef FDCN_STAMPS
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
-  for (int i = 0; i < kNumStamps; ++i) st_acc[i] = 0;
-  st_on = true;
-  (void)st_on;
-#endif
   for (int m = 0; m < A.n_time; ++m) {
     if (m == A.n_ranna && use_r) {  // Rannacher -> Crank-Nicolson
       ph = make_phase(0.5, dt, ca, cc, cbc);
@@ -980,7 +941,6 @@ fdcn_march(KArgs A) {
     const double lo_new = read_lane(bnd_cur.x, m & 63);
     const double hi_new = read_lane(bnd_cur.y, m & 63);
 
-    FDCN_STAMP(st_acc, st_prev, 0);
     // ---- 1. rhs ------------------------------------------------------------
     if constexpr (IT) {
       // IT form: the reference step  A x = B V + dt lambda  (+ Dirichlet
@@ -1087,7 +1047,6 @@ fdcn_march(KArgs A) {
     if (shrt) V[NPT - 2] = 0.0;  // the phantom node's rhs
     }  // CN rhs
 
-    FDCN_STAMP(st_acc, st_prev, 1);
     // ---- 2. tridiagonal solve ---------------------------------------------
     if constexpr (kRec) {
       // one fused solve for both phases (a second, plain solve for the
@@ -1112,7 +1071,6 @@ fdcn_march(KArgs A) {
     } else {
       solve(ph, std::false_type{});
     }
-    FDCN_STAMP(st_acc, st_prev, 7);
     // Sherman-Morrison: x = y - (k y0 / (1 + k z0)) z over the first lz lanes
     // (lanes >= lz use g = 0 and read row lz-1, one broadcast address), fused
     // with the Ikonen-Toivanen update for IT.  Both tables are read from LDS
@@ -1143,13 +1101,12 @@ fdcn_march(KArgs A) {
         for (int k = 0; k < NPT; ++k) V[k] = 0.0;
       }
     }
-    FDCN_STAMP(st_acc, st_prev, 8);
     // ---- 3. early exercise / boundaries / knock-out ------------------------
     // IT and kRec: the update / knock-out and the next RHS at priority 1,
     // between pass 1 + scan (3) and pass 2 (0): config 2 11.99 -> 11.74 ms,
     // config 5 19.73 -> 18.41 ms (3 instead of 1: 18.65); kSplit lost 2 %
     // with it (tools/gpu_ab_n.sh)
-    if constexpr ((IT || kRec) && FDCN_PRIO > 0) __builtin_amdgcn_s_setprio(1);
+    if constexpr (IT || kRec) __builtin_amdgcn_s_setprio(1);
     const double cq = (m + 1 < A.n_ranna) ? 1.0 : 2.0;  // 1/theta of the next step (IT)
     (void)cq;
     // kRec: the correction only changes nodes of lanes < lz; on a knock-out
@@ -1355,18 +1312,10 @@ fdcn_march(KArgs A) {
     }
   }
 
-#ifdef FDCN_STAMPS
-  FDCN_STAMP(st_acc, st_prev, 0);  // IT/KO tail of the last step -> bucket 0
-  if (lane == 0 && wave == 0) {
-    for (int i = 0; i < kNumStamps; ++i) atomicAdd(&fdcn_stamps[i], st_acc[i]);
-    atomicAdd(&fdcn_stamps[kNumStamps], 1ull);
-  }
-#endif
   if constexpr (IT) {  // Dirichlet values of the last step (the loop kept only rhs terms)
     if (A.n_time > 0) {
-      const double tau = tau0 + (double)A.n_time * dt;
-      V0 = bnd_eval(lof, l0, l1, l2, l3, tau);
-      VN = bnd_eval(hif, h0, h1, h2, h3, tau);
+      V0 = bnd_eval(lof, l0, l1, l2, l3, tau_end);
+      VN = bnd_eval(hif, h0, h1, h2, h3, tau_end);
     }
   }
   // ---- store ---------------------------------------------------------------
@@ -1559,7 +1508,7 @@ int launch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
            const double* params, const int32_t* iparams, const double* v_init,
            const double* payoff, int32_t n_mon, const int32_t* mon_step,
            const double* mon_rebate, double* v_out, int32_t k_cap, double* workspace,
-           hipStream_t stream) {
+           int64_t workspace_bytes, hipStream_t stream) {
   int rc = validate_common(B, n_nodes, n_time, n_ranna);
   if (rc) return rc;
   if (B == 0) return FDCN_OK;
@@ -1571,6 +1520,14 @@ int launch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   const size_t lds = sizeof(double) * (size_t)lds_doubles(*v, lz);
   if (lds > kLdsLimit)
     return fail(FDCN_EINVAL, "LDS request %zu B too large (k_cap=%d)", lds, k_cap);
+  const size_t ws_bytes = ws_bytes_per_scen(*v, n_time, lz) * (size_t)B;
+  // the variant (and so the workspace) depends on B: a buffer planned for
+  // another batch size may be too small -- refuse rather than overrun it
+  if (workspace && (workspace_bytes < 0 || (size_t)workspace_bytes < ws_bytes))
+    return fail(FDCN_EINVAL,
+                "workspace of %lld B is smaller than the %zu B this launch needs (B=%d, "
+                "W=%d, NPT=%d): size it with fdcn_plan for the same B and k_cap",
+                (long long)workspace_bytes, ws_bytes, B, v->w, v->npt);
   KArgs a;
   a.B = B;
   a.n_nodes = n_nodes;
@@ -1586,7 +1543,6 @@ int launch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   a.mon_rebate = mon_rebate;
   a.v_out = v_out;
   a.n_pad = pad64(n_time);
-  const size_t ws_bytes = ws_bytes_per_scen(*v, n_time, lz) * (size_t)B;
   bool own_ws = false;
   if (!workspace) {  // stream-ordered scratch, released after the launch
     HIP_TRY(hipMallocAsync((void**)&workspace, ws_bytes, stream));
@@ -1605,6 +1561,30 @@ int launch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
   return FDCN_OK;
 }
 
+// One non-blocking stream per (calling thread, device), created on first
+// use: host-array calls from different threads never share a stream or wait
+// for each other, and nothing is synchronised device-wide.  The device's
+// default memory pool keeps freed blocks (release threshold = max), so the
+// per-call stream-ordered allocations below are pool hits after warm-up.
+int thread_stream(hipStream_t* out) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  thread_local std::vector<hipStream_t> streams;
+  if ((size_t)dev >= streams.size()) streams.resize((size_t)dev + 1, nullptr);
+  if (!streams[dev]) {
+    HIP_TRY(hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking));
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
+  *out = streams[dev];
+  return FDCN_OK;
+}
+
+size_t align256(size_t n) { return (n + 255) / 256 * 256; }
+
 int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                const double* params, const int32_t* iparams, const double* v_init,
                const double* payoff, int32_t n_mon, const int32_t* mon_step,
@@ -1614,6 +1594,7 @@ int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ran
   if (!params || !iparams || !v_init || !v_out || (it && !payoff))
     return fail(FDCN_EINVAL, "null array argument");
   if (n_mon < 0) return fail(FDCN_EINVAL, "n_mon must be >= 0");
+  if (n_mon > 0 && (!mon_step || !mon_rebate)) return fail(FDCN_EINVAL, "null monitor arrays");
   for (int32_t b = 0; b < B; ++b) {
     const int32_t* I = iparams + (size_t)b * FDCN_NIPARAM;
     const int s = I[FDCN_I_MON_START], c = I[FDCN_I_MON_COUNT];
@@ -1621,8 +1602,17 @@ int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ran
       return fail(FDCN_EINVAL, "scenario %d: monitor range [%d,+%d) outside n_mon=%d", b, s, c,
                   n_mon);
     if (it && c != 0) return fail(FDCN_EINVAL, "scenario %d: IT solves take no monitors", b);
+    for (int k = 0; k < c; ++k) {
+      const int32_t st = mon_step[s + k];
+      if (st < 1 || st > n_time || (k > 0 && st <= mon_step[s + k - 1]))
+        return fail(FDCN_EINVAL,
+                    "scenario %d: monitor steps must be strictly increasing in [1, n_time=%d] "
+                    "(entry %d is %d)", b, n_time, k, st);
+    }
     for (int f = FDCN_I_LO_FORM; f <= FDCN_I_HI_FORM; ++f)
       if (I[f] != 0 && I[f] != 1) return fail(FDCN_EINVAL, "scenario %d: bad boundary form", b);
+    if (I[FDCN_I_TAU_MODE] != 0 && I[FDCN_I_TAU_MODE] != 1)
+      return fail(FDCN_EINVAL, "scenario %d: TAU_MODE must be 0 or 1", b);
     const double dt = params[(size_t)b * FDCN_NPARAM + FDCN_P_DT];
     if (!(dt > 0.0) && n_time > 0) return fail(FDCN_EINVAL, "scenario %d: dt must be > 0", b);
   }
@@ -1632,66 +1622,61 @@ int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ran
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(FDCN_ENODEV, "no HIP device visible");
+  int32_t w_, npt_, spb_, lds_;
+  int64_t ws_ = 0;
+  rc = fdcn_plan(B, n_nodes, n_time, it, k_cap, &w_, &npt_, &spb_, &lds_, &ws_);
+  if (rc) return rc;
+  hipStream_t stream;
+  rc = thread_stream(&stream);
+  if (rc) return rc;
+
+  // one stream-ordered block for every device array of the call
   const size_t nv = (size_t)B * n_nodes;
-  double *dP = nullptr, *dV = nullptr, *dO = nullptr, *dF = nullptr, *dR = nullptr;
-  int32_t *dI = nullptr, *dM = nullptr;
-  auto cleanup = [&]() {
-    if (dP) (void)hipFree(dP);
-    if (dV) (void)hipFree(dV);
-    if (dO) (void)hipFree(dO);
-    if (dF) (void)hipFree(dF);
-    if (dR) (void)hipFree(dR);
-    if (dI) (void)hipFree(dI);
-    if (dM) (void)hipFree(dM);
-  };
-#define ALLOC(p, bytes)                                                        \
-  if (hipMalloc((void**)&(p), (bytes)) != hipSuccess) {                        \
-    cleanup();                                                                 \
-    return fail(FDCN_ENOMEM, "hipMalloc(%zu) failed", (size_t)(bytes));        \
-  }
-  ALLOC(dP, sizeof(double) * (size_t)B * FDCN_NPARAM);
-  ALLOC(dI, sizeof(int32_t) * (size_t)B * FDCN_NIPARAM);
-  ALLOC(dV, sizeof(double) * nv);
-  ALLOC(dO, sizeof(double) * nv);
-  if (it) ALLOC(dF, sizeof(double) * nv);
-  ALLOC(dM, sizeof(int32_t) * (size_t)(n_mon > 0 ? n_mon : 1));
-  ALLOC(dR, sizeof(double) * (size_t)(n_mon > 0 ? n_mon : 1));
-#undef ALLOC
-  hipError_t e = hipSuccess;
-  e = hipMemcpy(dP, params, sizeof(double) * (size_t)B * FDCN_NPARAM, hipMemcpyHostToDevice);
+  const size_t nm = (size_t)(n_mon > 0 ? n_mon : 1);
+  const size_t oP = 0;
+  const size_t oI = oP + align256(sizeof(double) * (size_t)B * FDCN_NPARAM);
+  const size_t oV = oI + align256(sizeof(int32_t) * (size_t)B * FDCN_NIPARAM);
+  const size_t oO = oV + align256(sizeof(double) * nv);
+  const size_t oF = oO + align256(sizeof(double) * nv);
+  const size_t oM = oF + (it ? align256(sizeof(double) * nv) : 0);
+  const size_t oR = oM + align256(sizeof(int32_t) * nm);
+  const size_t oW = oR + align256(sizeof(double) * nm);
+  const size_t ws_bytes = (size_t)ws_ * (size_t)B;
+  const size_t total = oW + align256(ws_bytes > 0 ? ws_bytes : 1);
+  char* blk = nullptr;
+  hipError_t e = hipMallocAsync((void**)&blk, total, stream);
+  if (e != hipSuccess)
+    return fail(FDCN_ENOMEM, "hipMallocAsync(%zu) failed: %s", total, hipGetErrorString(e));
+  double* dP = (double*)(blk + oP);
+  int32_t* dI = (int32_t*)(blk + oI);
+  double* dV = (double*)(blk + oV);
+  double* dO = (double*)(blk + oO);
+  double* dF = it ? (double*)(blk + oF) : nullptr;
+  int32_t* dM = (int32_t*)(blk + oM);
+  double* dR = (double*)(blk + oR);
+  double* dW = (double*)(blk + oW);
+  const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+  e = hipMemcpyAsync(dP, params, sizeof(double) * (size_t)B * FDCN_NPARAM, h2d, stream);
   if (e == hipSuccess)
-    e = hipMemcpy(dI, iparams, sizeof(int32_t) * (size_t)B * FDCN_NIPARAM,
-                  hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(dV, v_init, sizeof(double) * nv, hipMemcpyHostToDevice);
-  if (e == hipSuccess && it) e = hipMemcpy(dF, payoff, sizeof(double) * nv, hipMemcpyHostToDevice);
+    e = hipMemcpyAsync(dI, iparams, sizeof(int32_t) * (size_t)B * FDCN_NIPARAM, h2d, stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dV, v_init, sizeof(double) * nv, h2d, stream);
+  if (e == hipSuccess && it) e = hipMemcpyAsync(dF, payoff, sizeof(double) * nv, h2d, stream);
   if (e == hipSuccess && n_mon > 0)
-    e = hipMemcpy(dM, mon_step, sizeof(int32_t) * (size_t)n_mon, hipMemcpyHostToDevice);
+    e = hipMemcpyAsync(dM, mon_step, sizeof(int32_t) * (size_t)n_mon, h2d, stream);
   if (e == hipSuccess && n_mon > 0)
-    e = hipMemcpy(dR, mon_rebate, sizeof(double) * (size_t)n_mon, hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    cleanup();
-    return fail(FDCN_EHIP, "hipMemcpy H2D failed: %s", hipGetErrorString(e));
-  }
-  double* dW = nullptr;
-  {
-    int32_t w_, npt_, spb_, lds_;
-    int64_t ws_ = 0;
-    rc = fdcn_plan(B, n_nodes, n_time, it, k_cap, &w_, &npt_, &spb_, &lds_, &ws_);
-    if (rc == FDCN_OK && ws_ > 0 && hipMalloc((void**)&dW, (size_t)ws_ * B) != hipSuccess) {
-      cleanup();
-      return fail(FDCN_ENOMEM, "hipMalloc(workspace) failed");
-    }
-  }
+    e = hipMemcpyAsync(dR, mon_rebate, sizeof(double) * (size_t)n_mon, h2d, stream);
+  if (e != hipSuccess) rc = fail(FDCN_EHIP, "hipMemcpyAsync H2D failed: %s", hipGetErrorString(e));
   if (rc == FDCN_OK)
     rc = launch(it, B, n_nodes, n_time, n_ranna, dP, dI, dV, dF, n_mon, dM, dR, dO, k_cap, dW,
-                nullptr);
+                (int64_t)ws_bytes, stream);
   if (rc == FDCN_OK) {
-    e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(v_out, dO, sizeof(double) * nv, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) rc = fail(FDCN_EHIP, "kernel/D2H failed: %s", hipGetErrorString(e));
+    e = hipMemcpyAsync(v_out, dO, sizeof(double) * nv, hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) rc = fail(FDCN_EHIP, "hipMemcpyAsync D2H failed: %s", hipGetErrorString(e));
   }
-  if (dW) (void)hipFree(dW);
-  cleanup();
+  (void)hipFreeAsync(blk, stream);
+  e = hipStreamSynchronize(stream);
+  if (rc == FDCN_OK && e != hipSuccess)
+    rc = fail(FDCN_EHIP, "kernel / copies failed: %s", hipGetErrorString(e));
   return rc;
 }
 
@@ -1744,17 +1729,19 @@ int fdcn_plan(int32_t B, int32_t n_nodes, int32_t n_time, int32_t it_mode, int32
 int fdcn_cn_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                       const double* params, const int32_t* iparams, const double* v_init,
                       int32_t n_mon, const int32_t* mon_step, const double* mon_rebate,
-                      double* v_out, int32_t k_cap, double* workspace, void* stream) {
+                      double* v_out, int32_t k_cap, double* workspace, int64_t workspace_bytes,
+                      void* stream) {
   return launch(0, B, n_nodes, n_time, n_ranna, params, iparams, v_init, nullptr, n_mon,
-                mon_step, mon_rebate, v_out, k_cap, workspace, (hipStream_t)stream);
+                mon_step, mon_rebate, v_out, k_cap, workspace, workspace_bytes,
+                (hipStream_t)stream);
 }
 
 int fdcn_it_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                       const double* params, const int32_t* iparams, const double* v_init,
                       const double* payoff, double* v_out, int32_t k_cap, double* workspace,
-                      void* stream) {
+                      int64_t workspace_bytes, void* stream) {
   return launch(1, B, n_nodes, n_time, n_ranna, params, iparams, v_init, payoff, 0, nullptr,
-                nullptr, v_out, k_cap, workspace, (hipStream_t)stream);
+                nullptr, v_out, k_cap, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int fdcn_cn_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
@@ -1845,18 +1832,20 @@ int fdcn_device_count(void) {
 
 int fdcn_abi_version(void) { return FDCN_ABI_VERSION; }
 
-#ifdef FDCN_STAMPS
-// Diagnostic build only: copy (and with reset != 0, zero) the per-phase cycle
-// sums; out[kNumStamps] is the number of waves that contributed.
-int fdcn_debug_stamps(unsigned long long* out, int reset) {
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(fdcn_stamps), sizeof(fdcn_stamps)));
-  if (reset) {
-    unsigned long long z[kNumStamps + 1] = {0};
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(fdcn_stamps), z, sizeof(z)));
-  }
-  return kNumStamps;
+int fdcn_select_device(int32_t ordinal) {
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (ordinal < 0 || ordinal >= n)
+    return fail(FDCN_EINVAL, "device ordinal %d outside [0, %d)", ordinal, n);
+  HIP_TRY(hipSetDevice(ordinal));
+  return FDCN_OK;
 }
-#endif
+
+int fdcn_current_device(void) {
+  int d = -1;
+  if (hipGetDevice(&d) != hipSuccess) return fail(FDCN_EHIP, "hipGetDevice failed");
+  return d;
+}
+
 
 }  // extern "C"

@@ -10,6 +10,7 @@ few hundred bytes per scenario, so these calls are latency-bound.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple, TypeVar
 
 T = TypeVar("T")
@@ -23,11 +24,47 @@ def _dist():
     return dist if dist.is_available() and dist.is_initialized() else None
 
 
+def is_initialized() -> bool:
+    return _dist() is not None
+
+
 def rank_world() -> Tuple[int, int]:
     d = _dist()
     if d is None:
         return 0, 1
     return d.get_rank(), d.get_world_size()
+
+
+def local_rank() -> int:
+    """This process's GPU ordinal on its node: LOCAL_RANK as torch.distributed.run
+    exports it (0 when unset)."""
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def bind_device() -> Optional[int]:
+    """One process per GPU: make GPU `local_rank()` current for libfdcn (the
+    host-array entry points run on the calling thread's HIP device) and for
+    torch (RCCL collectives need it).  Returns the ordinal, or None on a host
+    with no gfx950 device (CPU tests over gloo).  Raises if the rank has no
+    GPU of its own -- every rank marching on GPU 0 is the failure this guards."""
+    from . import capi
+    try:
+        n = capi.device_count()
+    except capi.FdcnError:
+        return None
+    if n == 0:
+        return None
+    lr = local_rank()
+    if lr >= n:
+        raise capi.FdcnError(f"LOCAL_RANK={lr} but only {n} gfx950 device(s) are visible")
+    capi.select_device(lr)
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.set_device(lr)
+    except ImportError:  # pragma: no cover - torch is always present here
+        pass
+    return lr
 
 
 def shard_range(n: int, rank: Optional[int] = None, world: Optional[int] = None) -> range:

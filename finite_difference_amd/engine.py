@@ -171,17 +171,37 @@ class HipBackend:
 
 
 class Engine:
-    """Batches solves into launches on a backend (default: the HIP library)."""
+    """Batches solves into launches on a backend (default: the HIP library).
 
-    def __init__(self, backend=None):
+    Groups of different shapes are independent launches: with the HIP backend
+    they are issued from one host thread each, so they run concurrently on
+    the GPU (libfdcn gives every calling thread its own stream; ctypes drops
+    the GIL for the call).  A trade whose solves need two step counts -- the
+    American Richardson pair N / 2N -- then costs the longer march, not the
+    sum of both."""
+
+    def __init__(self, backend=None, concurrent: bool = True):
         self.backend = backend if backend is not None else HipBackend()
+        self.concurrent = concurrent
         self.launches = 0
         self.solves = 0
 
+    def _run_groups(self, groups: List[Group]) -> List[np.ndarray]:
+        if len(groups) < 2 or not self.concurrent or not isinstance(self.backend, HipBackend):
+            return [self.backend.run_group(g) for g in groups]
+        from concurrent.futures import ThreadPoolExecutor
+        dev = capi.current_device()  # the HIP device is per thread: carry it over
+
+        def one(g: Group) -> np.ndarray:
+            capi.select_device(dev)
+            return self.backend.run_group(g)
+        with ThreadPoolExecutor(max_workers=min(len(groups), 8)) as ex:
+            return list(ex.map(one, groups))
+
     def run(self, solves: Sequence[Solve]) -> List[np.ndarray]:
         out: List[Optional[np.ndarray]] = [None] * len(solves)
-        for g in group_solves(solves):
-            res = self.backend.run_group(g)
+        groups = group_solves(solves)
+        for g, res in zip(groups, self._run_groups(groups)):
             self.launches += 1
             self.solves += g.B
             for row, i in enumerate(g.index):

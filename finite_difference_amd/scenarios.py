@@ -219,6 +219,8 @@ def run_all_scenarios(config_csv_path: str, output_csv_path: Optional[str],
     from . import distributed
     cfg = pd.read_csv(config_csv_path)
     rows = [dict(r) for _, r in cfg.iterrows()]
+    if distributed.is_initialized():
+        distributed.bind_device()  # this rank's GPU (LOCAL_RANK), before any launch
     mine = distributed.shard(rows)
     res = run_rows_batched(mine, base_params, engine)
     res = distributed.gather_rows(res)
@@ -285,6 +287,8 @@ def run_all_american_scenarios(config_csv_path: str, output_csv_path: Optional[s
     import pandas as pd
     from . import distributed
     cfg = pd.read_csv(config_csv_path)
+    if distributed.is_initialized():
+        distributed.bind_device()
     rows = distributed.shard([dict(r) for _, r in cfg.iterrows()])
     pricers = [make_american_pricer(r["S0"], r["K"], r["sigma"], r["rate"], engine=engine,
                                     **base_params) for r in rows]

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define FDCN_ABI_VERSION 3
+#define FDCN_ABI_VERSION 4
 
 /* ---- per-scenario fp64 parameters: params[b*FDCN_NPARAM + k] ---------- */
 enum fdcn_param {
@@ -70,10 +70,15 @@ enum fdcn_iparam {
   FDCN_I_KO_LO,       /* monitor steps set V_j = rebate for j <= KO_LO (-1: none) */
   FDCN_I_KO_HI,       /* … and for j >= KO_HI (>= n_nodes: none)                 */
   FDCN_I_MON_START,   /* offset of this scenario's entries in mon_step/mon_rebate */
-  FDCN_I_MON_COUNT,   /* number of entries (sorted ascending, values in 1..n_time) */
-  FDCN_I_TAU_MODE,    /* 0: tau0+(m+1)*dt.  1: tau accumulated by repeated +dt as
-                         fd_american_equity.py:664-724 does.  The GPU engine always
-                         uses form 0 (ulp-level difference). */
+  FDCN_I_MON_COUNT,   /* number of entries: strictly increasing, values in 1..n_time
+                         (the host entry points return FDCN_EINVAL otherwise; the
+                         _dev kernels skip entries < 1 and entries not above the
+                         previous one, as the oracle does) */
+  FDCN_I_TAU_MODE,    /* tau after step m: 0: tau0 + (m+1)*dt (…pricer.py:519).
+                         1: tau accumulated by repeated tau = tau + dt, as
+                         fd_american_equity.py:664-724 does.  Both are honoured on
+                         the device; any other value is FDCN_EINVAL (host entry
+                         points) / treated as 0 (_dev). */
   FDCN_NIPARAM
 };
 
@@ -109,6 +114,12 @@ int fdcn_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                   const double* v_init, const double* payoff,
                   double* v_out);
 
+/* Threading: the host-pointer entry points are reentrant.  Each calling
+ * thread gets its own non-blocking HIP stream on the current device
+ * (fdcn_select_device / hipSetDevice), device buffers come stream-ordered
+ * from the device's memory pool, and the call waits on its own stream only
+ * (never a device-wide synchronisation). */
+
 /* ---- device-pointer entry points (all pointers are device memory) ----- */
 /* `stream` is a hipStream_t (NULL = default stream); the call is
  * asynchronous on that stream and performs no host sync.  Inputs and output
@@ -116,21 +127,27 @@ int fdcn_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
  * `k_cap` bounds the boundary-layer correction table (see fdcn_sm_extent);
  * pass the value fdcn_sm_extent returns for the same params.  A scenario whose
  * extent exceeds k_cap gets NaN outputs (loud, never silently wrong).
- * `workspace` is device scratch of B * ws_bytes_per_scen bytes as reported by
- * fdcn_plan for the same (n_nodes, n_time, mode, k_cap): the Dirichlet values
- * of every step are evaluated there once per launch.  With NULL the library
- * allocates it stream-ordered (hipMallocAsync/hipFreeAsync on `stream`);
- * pass a buffer to keep the call allocation-free (e.g. for hipGraph capture). */
+ * `workspace` is device scratch of `workspace_bytes` bytes, at least
+ * B * ws_bytes_per_scen as reported by fdcn_plan for the SAME B, n_nodes,
+ * n_time, mode and k_cap (the kernel variant, and with it the workspace,
+ * depends on B: small batches spread a scenario over more waves).  A smaller
+ * (or negative) workspace_bytes is rejected with FDCN_EINVAL.  The Dirichlet
+ * values of every step are evaluated there once per launch.  With NULL the
+ * library allocates it stream-ordered (hipMallocAsync/hipFreeAsync on
+ * `stream`, workspace_bytes ignored); pass a buffer to keep the call
+ * allocation-free (e.g. for hipGraph capture). */
 int fdcn_cn_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                       const double* params, const int32_t* iparams,
                       const double* v_init,
                       int32_t n_mon, const int32_t* mon_step, const double* mon_rebate,
-                      double* v_out, int32_t k_cap, double* workspace, void* stream);
+                      double* v_out, int32_t k_cap, double* workspace,
+                      int64_t workspace_bytes, void* stream);
 
 int fdcn_it_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                       const double* params, const int32_t* iparams,
                       const double* v_init, const double* payoff,
-                      double* v_out, int32_t k_cap, double* workspace, void* stream);
+                      double* v_out, int32_t k_cap, double* workspace,
+                      int64_t workspace_bytes, void* stream);
 
 /* ---- launch planning / introspection ---------------------------------- */
 /* Writes the kernel geometry a launch of B scenarios uses: waves per
@@ -205,6 +222,11 @@ int fdcn_dividend_jump(int32_t n, const double* s, const double* v, double cash_
 const char* fdcn_last_error(void);
 int fdcn_device_count(void);   /* gfx950 devices visible; 0 if none          */
 int fdcn_abi_version(void);    /* FDCN_ABI_VERSION                           */
+/* Make `ordinal` the calling thread's current HIP device (hipSetDevice): the
+ * host-pointer entry points run there.  One process per GPU calls it once
+ * with its local rank.  Returns FDCN_OK or FDCN_EINVAL / FDCN_EHIP. */
+int fdcn_select_device(int32_t ordinal);
+int fdcn_current_device(void); /* the calling thread's device, or < 0 on error */
 
 #ifdef __cplusplus
 }

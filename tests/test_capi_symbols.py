@@ -27,16 +27,28 @@ def test_library_exports_all_symbols():
 def test_abi_version_and_plan_without_gpu():
     L = capi.lib()
     assert L.fdcn_abi_version() == capi.ABI_VERSION
-    p = capi.plan(2049, True)
+    p = capi.plan(2049, True, B=4096)
     assert p["waves"] >= 1 and p["npt"] * 64 * p["waves"] >= 2047
-    p = capi.plan(1024, False)
+    p = capi.plan(1024, False, B=10000)
     assert p["npt"] * 64 * p["waves"] >= 1022
+
+
+def test_plan_depends_on_batch_size():
+    """The variant, and with it the workspace, depends on B: a workspace
+    planned for a large batch is too small for a single solve of the same
+    grid (the _dev entry points reject it, see test_gpu_boundary.py)."""
+    big = capi.plan(4097, False, n_time=4096, B=4096)
+    one = capi.plan(4097, False, n_time=4096, B=1)
+    assert (big["waves"], one["waves"]) == (1, 4)
+    assert one["ws_bytes_per_scen"] > big["ws_bytes_per_scen"]
 
 
 def test_invalid_size_reports_error():
     import pytest
     with pytest.raises(capi.FdcnError):
-        capi.plan(3, False)
+        capi.plan(3, False, B=1)
+    with pytest.raises(TypeError):
+        capi.plan(2049, True)  # B is required
 
 
 def test_log_grid_is_bitwise_math_exp():
@@ -53,3 +65,54 @@ def test_log_grid_is_bitwise_math_exp():
         ref_x = [x_min + i * dx for i in range(n + 1)]
         assert x.tolist() == ref_x
         assert s.tolist() == list(map(math.exp, ref_x))
+
+
+def _raw_cn(iparams, mon_step, n_time=10, B=1, n_nodes=20):
+    """fdcn_cn_batch straight through ctypes: argument validation happens
+    before any device is touched, so it is testable on a CPU-only host."""
+    import numpy as np
+    P = np.zeros((B, capi.NPARAM))
+    P[:, capi.P_DT] = 0.01
+    I = np.ascontiguousarray(np.asarray(iparams, dtype=np.int32).reshape(B, capi.NIPARAM))
+    V = np.zeros((B, n_nodes))
+    ms = np.ascontiguousarray(np.asarray(mon_step, dtype=np.int32))
+    mr = np.zeros(max(1, len(ms)))
+    out = np.empty_like(V)
+    rc = capi.lib().fdcn_cn_batch(B, n_nodes, n_time, 2, P.ctypes.data_as(capi._PD),
+                                  I.ctypes.data_as(capi._PI), V.ctypes.data_as(capi._PD),
+                                  len(ms), ms.ctypes.data_as(capi._PI),
+                                  mr.ctypes.data_as(capi._PD), out.ctypes.data_as(capi._PD))
+    return rc, capi.lib().fdcn_last_error().decode()
+
+
+def _ip(start=0, count=0, tau_mode=0):
+    return [0, 0, -1, 1 << 20, start, count, tau_mode]
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("steps", [[0, 3], [3, 3], [5, 2], [4, 11]],
+                         ids=["zero", "repeat", "descending", "beyond_n_time"])
+def test_host_entry_rejects_bad_monitor_steps(steps):
+    rc, msg = _raw_cn(_ip(0, len(steps)), steps)
+    assert rc == -1 and "monitor steps" in msg, (rc, msg)
+
+
+def test_host_entry_rejects_bad_tau_mode():
+    rc, msg = _raw_cn(_ip(tau_mode=2), [])
+    assert rc == -1 and "TAU_MODE" in msg, (rc, msg)
+
+
+def test_host_entry_accepts_valid_plan_until_the_device():
+    """A valid plan passes validation; without a GPU the call then fails with
+    FDCN_ENODEV (or runs, on a GPU host)."""
+    rc, msg = _raw_cn(_ip(0, 3, tau_mode=1), [1, 4, 10])
+    assert rc in (0, -3), (rc, msg)
+
+
+def test_select_device_without_gpu_is_an_error_not_a_crash():
+    if capi.device_count() > 0:
+        pytest.skip("GPU host")
+    rc = capi.lib().fdcn_select_device(0)
+    assert rc != 0

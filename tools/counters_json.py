@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""profiles/pmc_counters.json from tools/pmc_counters.sh output.
+
+Usage: python tools/counters_json.py TAG [WORKLOAD...]   (default: all three)
+
+Per workload, reads gpurun_out/<TAG>_<wl>/<pass>/*counter_collection.csv,
+sums each fdcn_march dispatch's rows per counter, averages over the
+dispatches, and records:
+  hbm_bytes_per_launch  FETCH_SIZE x 2 (gfx950 counts half of wide coalesced
+                        reads, MI355X_MICROARCH.md) + WRITE_SIZE, KiB -> B
+  valu_insts_per_launch SQ_INSTS_VALU (wave-level instructions)
+  gpu_clock_ghz         GRBM_GUI_ACTIVE / 8 XCDs / dispatch duration
+  valu_issue_utilisation  4 x SQ_INSTS_VALU / (1024 SIMDs x GUI cycles): a
+                        wave64 fp64 VALU op holds a 16-lane SIMD for 4 cycles
+plus the compulsory bytes the launch must move, and the sha of the kernel
+source the counters were measured on: bench.py reports these numbers only
+while fdcn_kernels.hip is unchanged.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+XCD = 8
+
+
+def per_launch(d):
+    per = defaultdict(lambda: defaultdict(float))
+    for f in glob.glob(os.path.join(d, "**", "*_counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if "fdcn_march" not in row["Kernel_Name"]:
+                continue
+            k = int(row["Dispatch_Id"])
+            per[k][row["Counter_Name"]] += float(row["Counter_Value"])
+            per[k]["_ns"] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+    if not per:
+        raise SystemExit(f"no fdcn_march rows under {d}")
+    acc = defaultdict(list)
+    for cs in per.values():
+        for c, v in cs.items():
+            acc[c].append(v)
+    return {c: sum(v) / len(v) for c, v in acc.items()}, len(per)
+
+
+def expected(wl):
+    import bench
+    from finite_difference_amd import capi
+    builder, ns, nt, is_it, label = bench.WORKLOADS[wl]
+    B = bench.DEFAULT_BATCH[wl]
+    g = builder(B, ns, nt, seed=0)
+    k_cap = capi.sm_extent(g.n_nodes, g.n_time, g.n_ranna, g.params)
+    plan = capi.plan(g.n_nodes, is_it, k_cap, n_time=g.n_time, B=g.B)
+    n_pad = (max(g.n_time, 1) + 63) // 64 * 64
+    waves = plan["waves"]
+    vec = g.B * g.n_nodes * 8
+    rd = g.params.nbytes + g.iparams.nbytes + vec * (2 if is_it else 1)
+    rd += len(g.mon_step) * 12
+    bnd = g.B * waves * n_pad * 16
+    ko_row = g.B * waves * plan["npt"] * 8 if (not is_it and plan["npt"] >= 48) else 0
+    rec = (g.B * 64 * plan["npt"] * 8 * min(g.n_ranna, g.n_time)
+           if (not is_it and waves == 1 and plan["npt"] > 40) else 0)
+    key = f"{label}_{ns}x{nt}_batch{B}"
+    node_steps = g.B * bench.node_units(g) * g.n_time
+    return key, rd + bnd + ko_row + rec, vec + bnd + ko_row + rec, plan, node_steps
+
+
+def main():
+    import bench
+    tag = sys.argv[1]
+    wls = sys.argv[2:] or ["american", "barrier", "double"]
+    path = os.path.join(ROOT, "profiles", "pmc_counters.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    for wl in wls:
+        base = os.path.join(ROOT, "gpurun_out", f"{tag}_{wl}")
+        fe, n1 = per_launch(os.path.join(base, "fetch"))
+        wr, n2 = per_launch(os.path.join(base, "write"))
+        sq, _ = per_launch(os.path.join(base, "sq"))
+        gr, _ = per_launch(os.path.join(base, "grbm"))
+        key, exp_rd, exp_wr, plan, node_steps = expected(wl)
+        rd, wb = fe["FETCH_SIZE"] * 2 * 1024, wr["WRITE_SIZE"] * 1024
+        clk = gr["GRBM_GUI_ACTIVE"] / XCD / gr["_ns"]
+        f64 = sum(gr.get(k, 0.0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64",
+                                            "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_TRANS_F64"))
+        out[key] = {
+            "kernel_src_sha": bench.kernel_src_sha(),
+            "hbm_bytes_per_launch": rd + wb,
+            "read_bytes": rd, "write_bytes": wb,
+            "expected_read_bytes": exp_rd, "expected_write_bytes": exp_wr,
+            "valu_insts_per_launch": sq["SQ_INSTS_VALU"],
+            "valu_insts_per_node_step": sq["SQ_INSTS_VALU"] / node_steps,
+            "valu_insts_per_wave": sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"],
+            "f64_valu_insts_per_launch": f64,
+            "fma_f64_per_launch": gr.get("SQ_INSTS_VALU_FMA_F64", 0.0),
+            "wait_inst_any_per_launch": sq.get("SQ_WAIT_INST_ANY"),
+            "lds_insts_per_launch": sq.get("SQ_INSTS_LDS"),
+            "gpu_clock_ghz": clk,
+            "profiled_launch_ms": gr["_ns"] * 1e-6,
+            "valu_issue_utilisation": 4.0 * sq["SQ_INSTS_VALU"] / (
+                gr["GRBM_GUI_ACTIVE"] / XCD * 256 * 4),
+            "plan": {"waves": plan["waves"], "npt": plan["npt"]},
+            "launches_averaged": min(n1, n2),
+            "source": (f"rocprofv3 --pmc, one counter group per pass, python bench.py "
+                       f"--workload {wl} --steps 2 --warmup 1 (tools/pmc_counters.sh {tag})"),
+        }
+        print(f"{key}: HBM {(rd + wb) / 1e6:.1f} MB (expected {(exp_rd + exp_wr) / 1e6:.1f}), "
+              f"VALU/node-step {out[key]['valu_insts_per_node_step']:.2f}, "
+              f"issue {out[key]['valu_issue_utilisation']:.2f} at {clk:.2f} GHz")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+        f.write("\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -6,7 +6,8 @@ set -o pipefail
 TAG=${1:-run}; shift || true
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -s -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s -p no:cacheprovider --timeout 120 \
+    --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?; echo "tests rc=$rc" >> gpurun_out/${TAG}_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py "$@" > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
