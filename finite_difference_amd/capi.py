@@ -35,7 +35,8 @@ EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batc
             "fdcn_rr_barrier_batch",
             "fdcn_rr_barrier_batch_dev", "fdcn_double_barrier_batch",
             "fdcn_double_barrier_batch_dev", "fdcn_last_error", "fdcn_device_count",
-            "fdcn_abi_version", "fdcn_select_device", "fdcn_current_device")
+            "fdcn_abi_version", "fdcn_select_device", "fdcn_current_device",
+            "fdcn_tau_sequence", "fdcn_tau_runs")
 RR_NPARAM, RR_NFLAG = 8, 5
 DB_NPARAM, DB_NFLAG = 8, 3
 
@@ -117,6 +118,10 @@ def lib() -> ctypes.CDLL:
             L.fdcn_device_count.argtypes = []
             L.fdcn_abi_version.restype = ctypes.c_int
             L.fdcn_abi_version.argtypes = []
+            L.fdcn_tau_sequence.restype = _I
+            L.fdcn_tau_sequence.argtypes = [ctypes.c_double, ctypes.c_double, _I, _V]
+            L.fdcn_tau_runs.restype = _I
+            L.fdcn_tau_runs.argtypes = [ctypes.c_double, ctypes.c_double, _I]
             L.fdcn_select_device.restype = ctypes.c_int
             L.fdcn_select_device.argtypes = [_I]
             L.fdcn_current_device.restype = ctypes.c_int
@@ -240,6 +245,21 @@ def log_grid(x_min: float, dx: float, n: int):
     s = np.empty(n + 1, dtype=np.float64)
     _check(lib().fdcn_log_grid(float(x_min), float(dx), int(n), x.ctypes.data, s.ctypes.data))
     return x, s
+
+
+def tau_sequence(tau0: float, dt: float, n: int) -> np.ndarray:
+    """tau after each of n steps of `tau = tau + dt` (FDCN_I_TAU_MODE = 1), as
+    the kernels evaluate it (host only)."""
+    out = np.empty(max(n, 0), dtype=np.float64)
+    _check(lib().fdcn_tau_sequence(float(tau0), float(dt), int(n), out.ctypes.data))
+    return out
+
+
+def tau_runs(tau0: float, dt: float, n: int) -> int:
+    rc = int(lib().fdcn_tau_runs(float(tau0), float(dt), int(n)))
+    if rc < 0:
+        _check(rc)
+    return rc
 
 
 def rr_barrier_batch(params, flags):

@@ -193,6 +193,60 @@ __host__ __device__ inline int sm_extent(double fm, int n_int) {
   return kk >= (double)n_int ? n_int : (int)kk;
 }
 
+// Accumulated tau (FDCN_I_TAU_MODE = 1): tau_{k+1} = fl(tau_k + dt), the
+// reference American loop's `tau = tau + dt` (fd_american_equity.py:664-724).
+// Within a binade [2^(e-1), 2^e) every tau_k is a multiple of the ulp u and
+// every add carries the same remainder r = dt - delta below u, so the rounded
+// increment delta is the same on every step -- unless |r| is exactly u/2
+// (ties-to-even then depends on tau_k's last bit).  There the sequence is
+// exactly tau_k0 + j delta (a multiple of u below 2^e is representable, so
+// that expression is exact with or without FMA contraction).  tau_next_run
+// walks the sequence run by run: one constant-increment run per binade, plus
+// single serial steps within 2 ulp of a binade crossing, at ties, and while
+// tau <= dt.  ~3 runs per binade instead of one dependent add per step, and
+// bit-identical to the serial adds (fdcn_tau_sequence exposes it to tests).
+struct TauRun {
+  int k, len;        // steps k .. k+len-1 advance tau_k -> tau_{k+len}
+  double t, delta;   // tau_k and the run's increment
+  double t_next;     // tau_{k+len}
+};
+
+__host__ __device__ inline bool tau_next_run(double& t, int& k, int n, double dt, TauRun& run) {
+#pragma clang fp contract(off)
+  if (k >= n) return false;
+  run.k = k;
+  run.t = t;
+  const double t1 = t + dt;  // one serial step unless a longer run is proven exact
+  run.len = 1;
+  run.delta = 0.0;
+  run.t_next = t1;
+  if (t >= 1e-300 && dt > 0.0 && dt < t && t1 < 1e300) {
+    int e;
+    (void)frexp(t, &e);                 // t in [2^(e-1), 2^e)
+    const double hi = ldexp(1.0, e);
+    const double u = ldexp(1.0, e - 53);  // ulp in that binade
+    const double delta = t1 - t;          // exact (Sterbenz: t <= t1 <= 2t)
+    const double r = dt - delta;          // exact, |r| <= u/2
+    if (t1 < hi && fabs(r) != 0.5 * u) {
+      // every add of the run stays below hi - u/2 if t + L delta <= hi - 2u
+      double L = (double)(n - k);
+      if (delta > 0.0) {
+        const double lim = floor((hi - 2.0 * u - t) / delta);
+        if (lim < L) L = lim;
+        while (L > 1.0 && t + L * delta > hi - 2.0 * u) L -= 1.0;
+      }
+      if (L >= 1.0) {
+        run.len = (int)L;
+        run.delta = delta;
+        run.t_next = t + L * delta;
+      }
+    }
+  }
+  t = run.t_next;
+  k += run.len;
+  return true;
+}
+
 // LDS exchange area for W > 1 (per scenario), in doubles.
 template <int W>
 struct Xch {
@@ -358,16 +412,21 @@ fdcn_march(KArgs A) {
   const int tau_mode = uni_i(I[FDCN_I_TAU_MODE]);
   double tau_end = tau0 + (double)A.n_time * dt;  // tau after the last step
   if (tau_mode == 1) {
-    // The accumulated sequence is inherently serial: every lane runs the
-    // same chain of adds (one per step, ~20 us for 4096 steps), and the
-    // owner lane of step m parks (tau_m, tau_{m-1}) in its workspace slot,
-    // which the tabulation below reads back before overwriting it.
+    // (tau_{m+1}, tau_m) of every step into the owner lane's workspace slot
+    // (read back by the same lane below), run by run (tau_next_run)
     double tc = tau0;
-    for (int m = 0; m < A.n_pad; ++m) {
-      const double tp = tc;
-      tc = tc + dt;
-      if (m + 1 == A.n_time) tau_end = tc;
-      if ((m & 63) == lane) bnd[m] = make_double2(tc, tp);
+    int kc = 0;
+    TauRun run;
+    while (tau_next_run(tc, kc, A.n_pad, dt, run)) {  // wave-uniform
+      if (run.k < A.n_time && A.n_time <= run.k + run.len)
+        tau_end = (A.n_time == run.k + run.len)
+                      ? run.t_next : run.t + (double)(A.n_time - run.k) * run.delta;
+      for (int m = run.k + ((lane - run.k) & 63); m < run.k + run.len; m += 64) {
+        const int j = m - run.k;
+        const double tp = run.t + (double)j * run.delta;
+        const double tn = (j + 1 == run.len) ? run.t_next : run.t + (double)(j + 1) * run.delta;
+        bnd[m] = make_double2(tn, tp);
+      }
     }
     __threadfence_block();
   }
@@ -1757,6 +1816,26 @@ int fdcn_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                   const double* payoff, double* v_out) {
   return host_batch(1, B, n_nodes, n_time, n_ranna, params, iparams, v_init, payoff, 0,
                     nullptr, nullptr, v_out);
+}
+
+int fdcn_tau_sequence(double tau0, double dt, int32_t n, double* tau) {
+  if (n < 0 || (n > 0 && !tau)) return fail(FDCN_EINVAL, "fdcn_tau_sequence: n >= 0, tau non-NULL");
+  double tc = tau0;
+  int kc = 0;
+  TauRun run;
+  while (tau_next_run(tc, kc, n, dt, run))
+    for (int j = 0; j < run.len; ++j)
+      tau[run.k + j] = (j + 1 == run.len) ? run.t_next : run.t + (double)(j + 1) * run.delta;
+  return FDCN_OK;
+}
+
+int fdcn_tau_runs(double tau0, double dt, int32_t n) {
+  if (n < 0) return fail(FDCN_EINVAL, "fdcn_tau_runs: n >= 0");
+  double tc = tau0;
+  int kc = 0, runs = 0;
+  TauRun run;
+  while (tau_next_run(tc, kc, n, dt, run)) ++runs;
+  return runs;
 }
 
 int fdcn_log_grid(double x_min, double dx, int32_t n, double* x, double* s) {

@@ -209,6 +209,15 @@ int fdcn_double_barrier_batch_dev(int32_t B, int32_t m, const double* params,
  * Returns FDCN_OK or FDCN_EINVAL (n < 0, s NULL). */
 int fdcn_log_grid(double x_min, double dx, int32_t n, double* x, double* s);
 
+/* The accumulated tau of FDCN_I_TAU_MODE = 1, as the kernels evaluate it:
+ * tau[m] = tau after step m of `tau = tau + dt` starting from tau0
+ * (fd_american_equity.py:664-724), m = 0..n-1.  Bit-identical to the serial
+ * adds; the device evaluates it in constant-increment runs (one per binade
+ * plus single steps at binade crossings and rounding ties) instead of n
+ * dependent adds.  fdcn_tau_runs returns the number of runs.  Host only. */
+int fdcn_tau_sequence(double tau0, double dt, int32_t n, double* tau);
+int fdcn_tau_runs(double tau0, double dt, int32_t n);
+
 /* Discrete-dividend jump between two American segments
  * (AmericanFDMPricer._apply_dividend_jump, fd_american_equity.py:732-772,
  * with the natural cubic spline of :479-553):

@@ -291,6 +291,49 @@ def gen_barrier():
         shutil.copy(os.path.join(REF, f), os.path.join(dst, f.replace(" ", "_space_")))
 
 
+def gen_double_out():
+    """The production engine's "double-out" branch (discrete_barrier_fdm_pricer.py
+    :435-437).  price_log2 raises for double-* (:946), so the fixtures pin the
+    march itself: _solve_grid(apply_KO=True) with both barriers, put and call,
+    with and without a rebate (paid at hit / discounted), parity-mode grids."""
+    m = load_barrier()
+    specs = [
+        dict(name="dko_call", spot=229.74, strike=220.0, sigma=0.25, option_type="call",
+             lower_barrier=205.0, upper_barrier=250.0, rate=0.07, num_time_steps=40),
+        dict(name="dko_put", spot=229.74, strike=235.0, sigma=0.30, option_type="put",
+             lower_barrier=210.0, upper_barrier=255.0, rate=0.073086, num_time_steps=50),
+        dict(name="dko_call_rebate_hit", spot=229.74, strike=225.0, sigma=0.28,
+             option_type="call", lower_barrier=200.0, upper_barrier=260.0, rate=0.07,
+             rebate_amount=1.5, rebate_at_hit=True, num_time_steps=45),
+        dict(name="dko_put_rebate_expiry", spot=229.74, strike=240.0, sigma=0.22,
+             option_type="put", lower_barrier=215.0, upper_barrier=245.0, rate=0.072,
+             rebate_amount=2.0, rebate_at_hit=False, num_time_steps=60),
+    ]
+    cases = []
+    for sp in specs:
+        kw = dict(sp)
+        name = kw.pop("name")
+        p = make_barrier(m, barrier_type="double-out", **kw)
+        rec = dict(name=name, inputs=dict(sp))
+        rec["V_ko"] = p._solve_grid(apply_KO=True)
+        rec["N_s"] = p.num_space_nodes
+        rec["S_min"], rec["S_max"] = p._S_min, p._S_max
+        rec["dx"] = p._build_log_grid()
+        rec["s_nodes"] = p.s_nodes
+        rec["monitor_idx"] = sorted(p._monitor_indices_tau(p.time_to_expiry /
+                                                           p.num_time_steps))
+        rec["attrs"] = dict(time_to_expiry=p.time_to_expiry,
+                            discount_rate_nacc=p.discount_rate_nacc,
+                            carry_rate_nacc=p.carry_rate_nacc, div_yield_nacc=p.div_yield_nacc)
+        try:
+            p.price_log2()
+            rec["price_log2_raises"] = None
+        except Exception as e:  # the reference refuses double-* here (:946)
+            rec["price_log2_raises"] = type(e).__name__
+        cases.append(rec)
+    dump("double_out_cases.json", dict(cases=cases))
+
+
 # --------------------------------------------------------------------------
 # 3. American engine
 # --------------------------------------------------------------------------
@@ -430,13 +473,15 @@ def gen_analytic():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["cn", "barrier", "american", "analytic", "black76"]
+    which = sys.argv[1:] or ["cn", "barrier", "double", "american", "analytic", "black76"]
     if "black76" in which:
         gen_black76()
     if "cn" in which:
         gen_cn_log()
     if "barrier" in which:
         gen_barrier()
+    if "double" in which:
+        gen_double_out()
     if "american" in which:
         gen_american(with_config2="config2" in which or not sys.argv[1:])
     if "analytic" in which:

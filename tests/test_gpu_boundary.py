@@ -103,15 +103,18 @@ def _launch_dev(it, g, t, ws, ws_bytes, k_cap, stream):
 
 @pytest.mark.parametrize("it", [True, False], ids=["it", "cn"])
 def test_dev_rejects_workspace_planned_for_another_batch(it):
-    """a workspace sized for a large batch is too small for a
-    4-scenario launch of the same grid (multi-wave variant): FDCN_EINVAL,
-    nothing launched; the right size runs and matches the oracle."""
+    """a workspace sized for another batch size (IT: a large batch's
+    plan is too small for a 4-scenario launch, which spreads each scenario
+    over 4 waves), or one double short, is refused with FDCN_EINVAL before
+    anything is launched; the right size runs and matches the oracle."""
     import torch
     g, t = _dev_setup(it)
     k_cap = capi.sm_extent(g.n_nodes, g.n_time, g.n_ranna, g.params)
-    wrong = capi.plan(g.n_nodes, it, k_cap, n_time=g.n_time, B=4096)["ws_bytes_per_scen"] * g.B
+    big = capi.plan(g.n_nodes, it, k_cap, n_time=g.n_time, B=4096)["ws_bytes_per_scen"] * g.B
     right = capi.plan(g.n_nodes, it, k_cap, n_time=g.n_time, B=g.B)["ws_bytes_per_scen"] * g.B
-    assert wrong < right
+    if it:  # IT: the large-batch plan (W=1) needs less than the 4-scenario one (W=4)
+        assert big < right
+    wrong = min(big, right - 8)
     ws = torch.empty(right // 8 + 1, dtype=torch.float64, device="cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
     with pytest.raises(capi.FdcnError, match="workspace"):
