@@ -14,8 +14,13 @@ march runs:
   by segment in lock-step, and cached, so the pair costs 2 launches instead
   of 8 sequential Python marches.
 
-Discrete dividends keep the reference's host-side natural-cubic-spline jump
-(fd_american_equity.py:479-553, 732-772) between segment launches.
+On the GPU (the default engine) ``price_log2`` / ``greeks_log2`` /
+``prefetch_many`` run in a device session (session.py): the segments of all
+grids march in lock-step launches, the discrete-dividend jump between
+segments (natural cubic spline, fd_american_equity.py:479-553, 732-772) runs
+on the device, and the Richardson / vega / theta epilogue (:925-1068) too;
+six numbers per trade come back.  With another engine (the CPU oracle in the
+tests) the host-side jump and epilogue below are used.
 """
 from __future__ import annotations
 
@@ -27,6 +32,7 @@ import numpy as np
 
 from . import capi, market
 from .engine import FORM_SUM, Boundary, Engine, Solve, default_engine, operator_coefficients
+from .session import GK_AMERICAN, GK_READOUT, Session, readout
 
 OptionType = Literal["call", "put"]
 
@@ -141,6 +147,7 @@ class AmericanFDMPricer:
 
         self.engine = engine
         self._cache: Dict[tuple, Tuple[np.ndarray, dict]] = {}
+        self._dev_cache: Dict[tuple, Dict[str, float]] = {}
 
     def _reset_trade(self, spot: float, strike: float, sigma: float) -> None:
         """Re-point this pricer at another trade with the same dates, curves,
@@ -482,6 +489,110 @@ class AmericanFDMPricer:
         self._restore(grid)
         return V.tolist()
 
+    # ------------------------------------------------- device (session) path
+    def _price2_ntime(self) -> int:
+        """Step count of price_log2's second grid: 2 * num_space_nodes (the
+        reference's quirk, fd_american_equity.py:950)."""
+        return 2 * self.num_space_nodes
+
+    def _theta_inputs(self) -> Tuple[float, float]:
+        """(spot, carry) of greeks_log2's theta identity (:1060-1068)."""
+        return self.spot, self.carry_rate_nacc
+
+    def _dev_key(self, dv_sigma: float) -> tuple:
+        return (float(dv_sigma), self._state_key(self.sigma, self.num_time_steps))
+
+    def _job_readout(self, job: dict, slot: int, cubic: bool):
+        """_interp_price (+ _local_cubic_delta_gamma) positions on a job's grid
+        (fd_american_equity.py:855-907): the snapped spot, and for the cubic
+        the node nearest to it clamped to [1, n-2]."""
+        st = job["grid"]
+        s = st["s_nodes"]
+        s0 = (st["spot_snapped"] if self.snap_spot_to_grid and st["spot_snapped"] is not None
+              else self.spot)
+        if not cubic:
+            return readout(slot, s, s0)
+        n = len(s) - 1
+        i = int(np.argmin(np.abs(np.asarray(s) - s0)))
+        i = 1 if i < 1 else (n - 2 if i > n - 2 else i)
+        return readout(slot, s, s0, s0, dg_mode=2, idx=i)
+
+    @staticmethod
+    def _march_jobs_device(jobs: list, engine: Engine, sess: Session) -> None:
+        """_march_jobs with the value vectors in HBM: segment i of every job in
+        lock-step launches (initial vectors: the payoff, then the previous
+        segment's slots), the dividend jumps on the device between segments.
+        Leaves each job's final slot in job["slot"]."""
+        n_seg = max(len(j["steps"]) for j in jobs)
+        for seg in range(n_seg):
+            solves, owners = [], []
+            for j in jobs:
+                if seg >= len(j["steps"]) or j["steps"][seg] < 1:
+                    continue
+                p = j["owner"]
+                sigma0, saved = p.sigma, p._grid_state()
+                try:
+                    p.sigma = j["sigma"]
+                    p._restore(j["grid"])
+                    if len(p.s_nodes) - 1 < 2:
+                        raise RuntimeError("Spatial grid too coarse.")
+                    restart = seg == 0 or (seg > 0 and p.option_type == "call")
+                    solves.append(p._segment_solve(j["v"], j["pts"][seg], j["pts"][seg + 1],
+                                                   j["steps"][seg], restart))
+                finally:
+                    p.sigma = sigma0
+                    p._restore(saved)
+                owners.append(j)
+            if solves:
+                vs = None if seg == 0 else [j["slot"] for j in owners]
+                for j, sl in zip(owners, engine.march_slots(sess, solves, vs)):
+                    j["slot"] = int(sl)
+            jump = [j for j in jobs if seg < len(j["divs"])]
+            by_n: Dict[int, list] = {}
+            for j in jump:
+                by_n.setdefault(len(j["grid"]["s_nodes"]), []).append(j)
+            for js in by_n.values():
+                S = np.array([j["grid"]["s_nodes"] for j in js], dtype=np.float64)
+                cash = [j["divs"][seg][1] for j in js]
+                kc = [(j["owner"]._strike_snapped_for(j) if j["owner"].option_type == "call"
+                       else -1.0) for j in js]
+                for j, sl in zip(js, sess.dividend_jump([j["slot"] for j in js], S, cash, kc)):
+                    j["slot"] = int(sl)
+
+    def _strike_snapped_for(self, job: dict) -> float:
+        st = job["grid"]
+        if self.snap_strike_to_grid and st["strike_snapped"] is not None:
+            return st["strike_snapped"]
+        return self.strike
+
+    def _device_requests(self, dv_sigma: float, price_only: bool):
+        N, s0, h = self.num_time_steps, self.sigma, dv_sigma
+        if price_only:
+            return [(s0, N), (s0, self._price2_ntime())]
+        return [(s0, N), (s0, 2 * N), (s0 + h, N), (s0 - h, N), (s0 + 2.0 * h, N),
+                (s0 - 2.0 * h, N), (s0, self._price2_ntime())]
+
+    def _device_jobs(self, requests) -> Tuple[list, List[int]]:
+        """One job per distinct (sigma, n_time) grid of `requests` and, per
+        request, the index of its job."""
+        keys, jobs, index = {}, [], []
+        sigma0, saved = self.sigma, self._grid_state()
+        try:
+            for sig, nt in requests:
+                key = self._state_key(sig, nt)
+                if key not in keys:
+                    self.sigma = float(sig)
+                    self._build_log_grid()
+                    divs, pts, steps = self._segments(int(nt))
+                    keys[key] = len(jobs)
+                    jobs.append(dict(owner=self, key=key, sigma=float(sig), grid=self._grid_state(),
+                                     divs=divs, pts=pts, steps=steps, v=self._payoff_array()))
+                index.append(keys[key])
+        finally:
+            self.sigma = sigma0
+            self._restore(saved)
+        return jobs, index
+
     # ----------------------------------------------------- price and greeks
     def _spot_for_interp(self) -> float:
         if self.snap_spot_to_grid and self.spot_snapped is not None:
@@ -522,6 +633,12 @@ class AmericanFDMPricer:
         """Richardson N vs 2*num_space_nodes (the reference's quirk, :950)."""
         if not use_richardson:
             return self.price_log(n_time=self.num_time_steps)
+        if self._engine().on_device:
+            hit = self._dev_cache.get(("price2",) + self._dev_key(0.0))
+            if hit is None:
+                greeks_many([self], price_only=True)
+                hit = self._dev_cache[("price2",) + self._dev_key(0.0)]
+            return hit["price_log2"]
         self.prefetch([(self.sigma, self.num_time_steps), (self.sigma, 2 * self.num_space_nodes)])
         p_n = self.price_log(n_time=self.num_time_steps)
         p_2n = self.price_log(n_time=2 * self.num_space_nodes)
@@ -550,6 +667,12 @@ class AmericanFDMPricer:
 
     def greeks_log2(self, dv_sigma: float = 0.01, use_richardson: bool = True) -> Dict[str, float]:
         """Price and Greeks as fd_american_equity.py:970-1068."""
+        if use_richardson and self._engine().on_device:
+            hit = self._dev_cache.get(self._dev_key(dv_sigma))
+            if hit is None:
+                greeks_many([self], dv_sigma)
+                hit = self._dev_cache[self._dev_key(dv_sigma)]
+            return {k: hit[k] for k in ("price", "delta", "gamma", "vega", "theta")}
         self.prefetch(self.greeks_requests(dv_sigma, use_richardson, with_price=False))
         v_n = self._solve_grid(n_time=self.num_time_steps)
         price_n = self._interp_price(v_n)
@@ -582,6 +705,50 @@ class AmericanFDMPricer:
                 "vega": float(vega), "theta": float(theta)}
 
 
+def greeks_many(pricers: Sequence[AmericanFDMPricer], dv_sigma: float = 0.01,
+                price_only: bool = False) -> None:
+    """price_log2 (+ greeks_log2 unless price_only) of many trades in one
+    device session: every trade's grids (N, 2N, sigma +-h, +-2h and price_log2's
+    second grid; dividend segments in lock-step with the spline jumps on the
+    device) march in shared launches, and the readouts, Richardson
+    extrapolations, vega and theta run on the device (FDCN_GK_AMERICAN);
+    six numbers per trade come back.  Results land in each pricer's cache."""
+    if not pricers:
+        return
+    engine = pricers[0]._engine()
+    jobs, plan = [], []
+    for p in pricers:
+        pj, idx = p._device_jobs(p._device_requests(dv_sigma, price_only))
+        plan.append((p, [len(jobs) + i for i in idx]))
+        jobs.extend(pj)
+    with Session() as S:
+        AmericanFDMPricer._march_jobs_device(jobs, engine, S)
+        trades = []
+        for p, ji in plan:
+            if price_only:
+                trades.append((GK_READOUT, [p._job_readout(jobs[ji[0]], jobs[ji[0]]["slot"], False)],
+                               ()))
+                trades.append((GK_READOUT, [p._job_readout(jobs[ji[1]], jobs[ji[1]]["slot"], False)],
+                               ()))
+                continue
+            rds = [p._job_readout(jobs[k], jobs[k]["slot"], cubic=(n < 2))
+                   for n, k in enumerate(ji)]
+            spot, carry = p._theta_inputs()
+            trades.append((GK_AMERICAN, rds, (p.sigma, spot, carry, p.discount_rate_nacc,
+                                              dv_sigma)))
+        out = S.greeks(trades)
+    for t, (p, ji) in enumerate(plan):
+        if price_only:
+            p_n, p_2 = float(out[2 * t, 0]), float(out[2 * t + 1, 0])
+            p._dev_cache[("price2",) + p._dev_key(0.0)] = {"price_log2": (4.0 * p_2 - p_n) / 3.0}
+            continue
+        o = out[t]
+        p._dev_cache[p._dev_key(dv_sigma)] = {
+            "price": float(o[0]), "delta": float(o[1]), "gamma": float(o[2]),
+            "vega": float(o[3]), "theta": float(o[4])}
+        p._dev_cache[("price2",) + p._dev_key(0.0)] = {"price_log2": float(o[5])}
+
+
 def prefetch_many(pricers: Sequence[AmericanFDMPricer], dv_sigma: float = 0.01,
                   use_richardson: bool = True) -> None:
     """Solve every grid that price_log2 + greeks_log2 of many trades will need.
@@ -593,6 +760,9 @@ def prefetch_many(pricers: Sequence[AmericanFDMPricer], dv_sigma: float = 0.01,
     extra segment, shared by every trade, with the host's spline jumps in
     between."""
     if not pricers:
+        return
+    if use_richardson and pricers[0]._engine().on_device:
+        greeks_many([p for p in pricers if p._dev_key(dv_sigma) not in p._dev_cache], dv_sigma)
         return
     jobs = []
     for p in pricers:

@@ -85,6 +85,15 @@ class AmericanFwdFDMPricer(AmericanFDMPricer):
     def _div_times_tau(self):
         return []
 
+    def _price2_ntime(self) -> int:
+        """price_log2 uses 2 * num_time_steps here (fd_american_black76.py:537-546)."""
+        return 2 * self.num_time_steps
+
+    def _theta_inputs(self):
+        """theta = -(1/2 sigma^2 F0^2 Gamma - r P) (fd_american_black76.py:620):
+        the spot form with zero carry."""
+        return self.forward0, 0.0
+
     # ----------------------------------------------------------- public API
     def _solve_grid(self, N_time: Optional[int] = None) -> List[float]:
         return super()._solve_grid(n_time=N_time)
@@ -96,6 +105,8 @@ class AmericanFwdFDMPricer(AmericanFDMPricer):
         """Richardson N vs 2N (fd_american_black76.py:537-546)."""
         if not use_richardson:
             return self.price_log(N_time=self.num_time_steps)
+        if self._engine().on_device:
+            return super().price_log2(apply_KO, use_richardson)
         self.prefetch([(self.sigma, self.num_time_steps), (self.sigma, 2 * self.num_time_steps)])
         p_n = self.price_log(N_time=self.num_time_steps)
         p_2n = self.price_log(N_time=2 * self.num_time_steps)
@@ -119,6 +130,8 @@ class AmericanFwdFDMPricer(AmericanFDMPricer):
 
     def greeks_log2(self, dv_sigma: float = 0.01, use_richardson: bool = True) -> Dict[str, float]:
         """Price and Greeks as fd_american_black76.py:556-625 (Delta/Gamma in F)."""
+        if use_richardson and self._engine().on_device:
+            return super().greeks_log2(dv_sigma, use_richardson)
         self.prefetch(self.greeks_requests(dv_sigma, use_richardson))
         N = self.num_time_steps
         v_n = self._solve_grid(N_time=N)

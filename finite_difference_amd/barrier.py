@@ -31,6 +31,7 @@ import numpy as np
 from . import capi, market
 from .engine import (FORM_PROD, FORM_SUM, Boundary, Engine, Solve, default_engine,
                      operator_coefficients)
+from .session import GK_BARRIER, Session, nearest_interior, readout
 
 BarrierType = Literal["down-and-out", "up-and-out", "double-out", "down-and-in", "up-and-in",
                       "double-in", "none"]
@@ -60,16 +61,9 @@ def tail_quantile() -> float:
 _MON_CACHE: Dict[tuple, frozenset] = {}
 
 
-def _nearest_interior(s: Sequence[float], x: float) -> int:
-    """1 + argmin_{1 <= i <= len(s)-2} |s_i - x| for increasing s (first
-    index on ties, as np.argmin), by bisection instead of a full scan."""
-    lo, hi = 1, len(s) - 2
-    j = bisect.bisect_left(s, x, lo, hi + 1)  # first i in [lo, hi+1) with s_i >= x
-    if j <= lo:
-        return lo
-    if j > hi:
-        return hi
-    return j - 1 if abs(s[j - 1] - x) <= abs(s[j] - x) else j
+# 1 + argmin_{1 <= i <= len(s)-2} |s_i - x| for increasing s (first index on
+# ties, as np.argmin), by bisection instead of a full scan
+_nearest_interior = nearest_interior
 
 
 def _norm_cdf(x: float) -> float:
@@ -578,15 +572,28 @@ class DiscreteBarrierFDMPricer:
         return {"price": price_base, "delta": delta, "gamma": gamma, "vega": vega,
                 "theta": theta}
 
+    def _device_spec(self, sb: Solve, gb: _Grid, su: Solve, gu: _Grid,
+                     dv_sigma: float) -> "DeviceTrade":
+        """What _pde_finish reads of this trade, captured now (batch runners
+        re-point one pricer at many rows before the launches finish)."""
+        return DeviceTrade(sb, gb, su, gu, self.spot - self.pv_divs, self.spot,
+                           (self.sigma, self.spot, self.carry_rate_nacc, self.div_yield_nacc,
+                            self.discount_rate_nacc, dv_sigma))
+
     def _pde_price_and_greeks3(self, apply_KO: bool, dv_sigma: float = 0.0001,
                                use_richardson: bool = False) -> Dict[str, float]:
-        """Base + bumped solve in one launch; cached (:883-904)."""
+        """Base + bumped solve in one launch; cached (:883-904).  On the GPU
+        the value vectors stay in HBM and only the five numbers come back."""
         key = self._pde_key(apply_KO, dv_sigma)
         hit = self._pde_cache.get(key)
         if hit is None:
             (sb, gb), (su, gu) = self.pde_solves(apply_KO, dv_sigma)
-            Vb, Vu = self._engine().run([sb, su])
-            hit = self._pde_finish(Vb, gb, Vu, gu, dv_sigma)
+            eng = self._engine()
+            if eng.on_device:
+                hit = finish_on_device(eng, [self._device_spec(sb, gb, su, gu, dv_sigma)])[0]
+            else:
+                Vb, Vu = eng.run([sb, su])
+                hit = self._pde_finish(Vb, gb, Vu, gu, dv_sigma)
             self._pde_cache[key] = hit
             self.s_nodes = gu.s_nodes  # the reference leaves the bumped grid behind
             self.num_space_nodes = gu.n_space
@@ -691,6 +698,41 @@ class DiscreteBarrierFDMPricer:
         return out
 
 
+GREEKS_KEYS = ("price", "delta", "gamma", "vega", "theta")
+
+
+class DeviceTrade:
+    """One trade's base / sigma-bumped solves and the scalars _pde_finish
+    uses (interpolation spot S0 = spot - PV(divs), Delta/Gamma spot, theta
+    and vega inputs), for the device epilogue (FDCN_GK_BARRIER)."""
+    __slots__ = ("sb", "gb", "su", "gu", "S0", "spot", "params")
+
+    def __init__(self, sb, gb, su, gu, S0, spot, params):
+        self.sb, self.gb, self.su, self.gu = sb, gb, su, gu
+        self.S0, self.spot, self.params = S0, spot, params
+
+    def trade(self, slot_b: int, slot_u: int) -> tuple:
+        """Readouts at the grid positions _interp_price / _delta_gamma_from_grid
+        use (:629-646, :949-978); the kernel keeps their operation order, so
+        on the same value vectors the numbers are the host epilogue's."""
+        rb = readout(slot_b, self.gb.s_arr, self.S0, self.spot, dg_mode=1, n_v=self.sb.n_nodes)
+        ru = readout(slot_u, self.gu.s_arr, self.S0, n_v=self.su.n_nodes)
+        return GK_BARRIER, [rb, ru], self.params
+
+
+def finish_on_device(engine: Engine, specs: Sequence[DeviceTrade]) -> List[Dict[str, float]]:
+    """March every trade's base and bumped solve in one device session and
+    run the Greeks epilogue there: only 6 numbers per trade cross PCIe."""
+    if not specs:
+        return []
+    solves = [x for d in specs for x in (d.sb, d.su)]
+    with Session() as S:
+        slots = engine.march_slots(S, solves)
+        out = S.greeks([d.trade(int(slots[2 * i]), int(slots[2 * i + 1]))
+                        for i, d in enumerate(specs)])
+    return [dict(zip(GREEKS_KEYS, map(float, row[:5]))) for row in out]
+
+
 def price_many(pricers: Sequence[DiscreteBarrierFDMPricer], dv_sigma: float = 0.0001) -> None:
     """Run the PDE solves of many trades together (one launch per grid shape)
     and fill each pricer's cache, so price_log2 / greeks_log2 return at once."""
@@ -711,15 +753,21 @@ def price_many(pricers: Sequence[DiscreteBarrierFDMPricer], dv_sigma: float = 0.
             if key in p._pde_cache:
                 continue
             (sb, gb), (su, gu) = p.pde_solves(True, dv_sigma)
+            spec = p._device_spec(sb, gb, su, gu, dv_sigma)
         finally:
             p.barrier_type = keep
-        todo.append((p, kbt, key, gb, gu))
+        todo.append((p, kbt, key, gb, gu, spec))
         solves.extend([sb, su])
     if not solves:
         return
     engine = pricers[0]._engine()
+    if engine.on_device:
+        outs = finish_on_device(engine, [t[5] for t in todo])
+        for (p, kbt, key, gb, gu, spec), hit in zip(todo, outs):
+            p._pde_cache[key] = hit
+        return
     res = engine.run(solves)
-    for i, (p, kbt, key, gb, gu) in enumerate(todo):
+    for i, (p, kbt, key, gb, gu, spec) in enumerate(todo):
         keep = p.barrier_type
         p.barrier_type = kbt
         try:

@@ -36,7 +36,9 @@ EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batc
             "fdcn_rr_barrier_batch_dev", "fdcn_double_barrier_batch",
             "fdcn_double_barrier_batch_dev", "fdcn_last_error", "fdcn_device_count",
             "fdcn_abi_version", "fdcn_select_device", "fdcn_current_device",
-            "fdcn_tau_sequence", "fdcn_tau_runs")
+            "fdcn_tau_sequence", "fdcn_tau_runs", "fdcn_session_create",
+            "fdcn_session_destroy", "fdcn_session_slots", "fdcn_session_march",
+            "fdcn_session_dividend_jump", "fdcn_session_greeks", "fdcn_session_fetch")
 RR_NPARAM, RR_NFLAG = 8, 5
 DB_NPARAM, DB_NFLAG = 8, 3
 

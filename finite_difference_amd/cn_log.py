@@ -28,6 +28,7 @@ import numpy as np
 from . import capi
 
 from .engine import FORM_SUM, Boundary, Engine, Solve, default_engine, operator_coefficients
+from .session import GK_CNLOG, Session, readout
 
 SQRT_2PI = math.sqrt(2.0 * math.pi)
 
@@ -261,7 +262,20 @@ class DiscreteBarrierCrankNicolsonLog:
         s0 = self.sigma
         solves = [self._make_solve(apply_KO, s0), self._make_solve(apply_KO, s0 + dv_sigma),
                   self._make_solve(apply_KO, s0 - dv_sigma)]
-        V, Vu, Vd = self._engine().run(solves)
+        eng = self._engine()
+        if eng.on_device:
+            # the three grids are one grid (configure_grid does not depend on
+            # sigma once N is set): read it on the device, 6 numbers come back
+            s = self.s_nodes
+            with Session() as S:
+                sl = eng.march_slots(S, solves)
+                rb = readout(int(sl[0]), s, self.S0, self.S0, dg_mode=1)
+                ru, rd = readout(int(sl[1]), s, self.S0), readout(int(sl[2]), s, self.S0)
+                o = S.greeks([(GK_CNLOG, [rb, ru, rd],
+                               (s0, self.S0, self.b_carry, self.r_disc, dv_sigma))])[0]
+            return {"price": float(o[0]), "delta": float(o[1]), "gamma": float(o[2]),
+                    "theta": float(o[4]), "vega": float(o[3])}
+        V, Vu, Vd = eng.run(solves)
         price = self._interp_price_from_grid(V)
         delta, gamma = self._delta_gamma_from_grid(V)
         theta = -(0.5 * s0 * s0 * self.S0 * self.S0 * gamma + self.b_carry * self.S0 * delta

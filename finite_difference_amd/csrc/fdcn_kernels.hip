@@ -1644,14 +1644,14 @@ int thread_stream(hipStream_t* out) {
 
 size_t align256(size_t n) { return (n + 255) / 256 * 256; }
 
-int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
-               const double* params, const int32_t* iparams, const double* v_init,
-               const double* payoff, int32_t n_mon, const int32_t* mon_step,
-               const double* mon_rebate, double* v_out) {
+// Host-side checks of a launch plan (host arrays): sizes, monitor runs
+// (strictly increasing, in [1, n_time]), boundary forms, tau mode, dt > 0.
+int validate_plan(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                  const double* params, const int32_t* iparams, int32_t n_mon,
+                  const int32_t* mon_step, const double* mon_rebate) {
   int rc = validate_common(B, n_nodes, n_time, n_ranna);
   if (rc) return rc;
-  if (!params || !iparams || !v_init || !v_out || (it && !payoff))
-    return fail(FDCN_EINVAL, "null array argument");
+  if (B > 0 && (!params || !iparams)) return fail(FDCN_EINVAL, "null array argument");
   if (n_mon < 0) return fail(FDCN_EINVAL, "n_mon must be >= 0");
   if (n_mon > 0 && (!mon_step || !mon_rebate)) return fail(FDCN_EINVAL, "null monitor arrays");
   for (int32_t b = 0; b < B; ++b) {
@@ -1675,6 +1675,18 @@ int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ran
     const double dt = params[(size_t)b * FDCN_NPARAM + FDCN_P_DT];
     if (!(dt > 0.0) && n_time > 0) return fail(FDCN_EINVAL, "scenario %d: dt must be > 0", b);
   }
+  return FDCN_OK;
+}
+
+int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+               const double* params, const int32_t* iparams, const double* v_init,
+               const double* payoff, int32_t n_mon, const int32_t* mon_step,
+               const double* mon_rebate, double* v_out) {
+  int rc = validate_plan(it, B, n_nodes, n_time, n_ranna, params, iparams, n_mon, mon_step,
+                         mon_rebate);
+  if (rc) return rc;
+  if (B > 0 && (!v_init || !v_out || (it && !payoff)))
+    return fail(FDCN_EINVAL, "null array argument");
   if (B == 0) return FDCN_OK;
   const int k_cap = fdcn_sm_extent(B, n_nodes, n_time, n_ranna, params);
   if (k_cap < 0) return k_cap;
@@ -1744,6 +1756,22 @@ int host_batch(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ran
 namespace fdcn_internal {
 // error reporting shared with the other translation units of libfdcn
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+// the march and its plan checks, for the session runtime (fdcn_session.hip)
+int validate_plan(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                  const double* params, const int32_t* iparams, int32_t n_mon,
+                  const int32_t* mon_step, const double* mon_rebate) {
+  return ::validate_plan(it, B, n_nodes, n_time, n_ranna, params, iparams, n_mon, mon_step,
+                         mon_rebate);
+}
+int launch_march(int it, int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                 const double* params, const int32_t* iparams, const double* v_init,
+                 const double* payoff, int32_t n_mon, const int32_t* mon_step,
+                 const double* mon_rebate, double* v_out, int32_t k_cap, double* workspace,
+                 int64_t workspace_bytes, hipStream_t stream) {
+  return launch(it, B, n_nodes, n_time, n_ranna, params, iparams, v_init, payoff, n_mon,
+                mon_step, mon_rebate, v_out, k_cap, workspace, workspace_bytes, stream);
+}
+int thread_stream(hipStream_t* out) { return ::thread_stream(out); }
 }  // namespace fdcn_internal
 
 // ---------------------------------------------------------------------------

@@ -198,6 +198,26 @@ class Engine:
         with ThreadPoolExecutor(max_workers=min(len(groups), 8)) as ex:
             return list(ex.map(one, groups))
 
+    @property
+    def on_device(self) -> bool:
+        """True for the HIP engine: the facades then keep value vectors in HBM
+        (session.Session) and run the Greeks epilogue there."""
+        return isinstance(self.backend, HipBackend)
+
+    def march_slots(self, sess, solves: Sequence[Solve],
+                    v_init_slots: Optional[Sequence[int]] = None) -> np.ndarray:
+        """Launch `solves` in `sess` (one launch per shape, overlapping on the
+        session's streams) and return the output slot of each solve.  With
+        v_init_slots, solve i starts from slot v_init_slots[i]."""
+        out = np.empty(len(solves), dtype=np.int32)
+        for g in group_solves(solves):
+            vs = None if v_init_slots is None else np.asarray(
+                [v_init_slots[i] for i in g.index], dtype=np.int32)
+            out[g.index] = sess.march(g, vs)
+            self.launches += 1
+            self.solves += g.B
+        return out
+
     def run(self, solves: Sequence[Solve]) -> List[np.ndarray]:
         out: List[Optional[np.ndarray]] = [None] * len(solves)
         groups = group_solves(solves)

@@ -174,7 +174,7 @@ def run_rows_batched(rows: List[dict], base_params: Dict[str, Any],
                        _opt(row, "lower_barrier"), _opt(row, "upper_barrier"))
         return p
 
-    plan, solves = [], []
+    plan, solves, specs = [], [], []
     for row in rows:
         p = pricer_for(row)
         bt = p.barrier_type.lower()
@@ -188,18 +188,25 @@ def run_rows_batched(rows: List[dict], base_params: Dict[str, Any],
             continue
         p.barrier_type = kbt
         (sb, gb), (su, gu) = p.pde_solves(True, dv_sigma)
+        specs.append(p._device_spec(sb, gb, su, gu, dv_sigma))
         plan.append((row, kbt, gb, gu, len(solves)))
         solves.extend([sb, su])
-    res = (engine if engine is not None else next(iter(calcs.values()))._engine()).run(solves) \
-        if solves else []
+    eng = engine if engine is not None else (
+        next(iter(calcs.values()))._engine() if calcs else None)
+    dev = None
+    if solves and eng.on_device:  # value vectors stay in HBM; 6 numbers per trade come back
+        from .barrier import finish_on_device
+        dev = iter(finish_on_device(eng, specs))
+    res = eng.run(solves) if solves and dev is None else []
     out = []
     for row, kbt, gb, gu, i in plan:
         p = pricer_for(row)
         if kbt is not None:
             keep = p.barrier_type
             p.barrier_type = kbt
-            p._pde_cache[p._pde_key(True, dv_sigma)] = p._pde_finish(res[i], gb, res[i + 1], gu,
-                                                                     dv_sigma)
+            p._pde_cache[p._pde_key(True, dv_sigma)] = (
+                next(dev) if dev is not None else
+                p._pde_finish(res[i], gb, res[i + 1], gu, dv_sigma))
             p.barrier_type = keep
         out.append(_barrier_row(row["scenario_name"], row["S0"], row["K"], row["sigma"],
                                 row["rate"], row["barrier_type"], _opt(row, "upper_barrier"),

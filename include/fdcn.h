@@ -149,6 +149,78 @@ int fdcn_it_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_rann
                       double* v_out, int32_t k_cap, double* workspace,
                       int64_t workspace_bytes, void* stream);
 
+/* ---- device-resident sessions (finite_difference_amd/csrc/fdcn_session.hip)
+ * A session keeps solve outputs in HBM as numbered "slots" (one value vector
+ * each) and chains marches, dividend jumps and the Greeks epilogue on the
+ * device; only what the caller asks for comes back.  It replaces the host
+ * round trips of
+ *   _solve_grid -> _interp_price / _delta_gamma_from_grid / greeks
+ *     (discrete_barrier_fdm_pricer.py:629-646, :883-904, :949-978;
+ *      discrete_barrier_fdm_pricer_cn.py:429-466; fd_american_equity.py:855-1068)
+ *   _solve_segment -> _apply_dividend_jump -> _solve_segment
+ *     (fd_american_equity.py:479-553, :732-772, :825-843).
+ * A session belongs to the thread's current device (fdcn_select_device) and is
+ * not thread-safe; use one per thread.  Marches and jumps are asynchronous
+ * (independent ones overlap on up to 4 session streams); greeks and fetch wait
+ * for their inputs and return results.  Host arrays are staged through pinned
+ * memory before a call returns.  After an error, destroy the session. */
+typedef struct fdcn_session fdcn_session;
+int fdcn_session_create(fdcn_session** out);
+int fdcn_session_destroy(fdcn_session* s);
+int fdcn_session_slots(const fdcn_session* s);  /* slots created so far */
+
+/* One batched march (the fdcn_cn_batch / fdcn_it_batch plan; it != 0 for
+ * Ikonen-Toivanen).  Initial vectors come from the host (v_init [B][n_nodes])
+ * or from earlier slots (v_init_slots [B]); pass exactly one.  The B outputs
+ * become new slots, numbers written to out_slots [B]. */
+int fdcn_session_march(fdcn_session* s, int32_t it, int32_t B, int32_t n_nodes, int32_t n_time,
+                       int32_t n_ranna, const double* params, const int32_t* iparams,
+                       const double* v_init, const int32_t* v_init_slots, const double* payoff,
+                       int32_t n_mon, const int32_t* mon_step, const double* mon_rebate,
+                       int32_t* out_slots);
+
+/* fdcn_dividend_jump of B slots on the device: s_nodes [B][n_nodes] (host),
+ * cash_div [B], strike_call [B] (< 0 for puts); results into new slots.
+ * Bit-identical to fdcn_dividend_jump on the same inputs. */
+int fdcn_session_dividend_jump(fdcn_session* s, int32_t B, int32_t n_nodes,
+                               const int32_t* in_slots, const double* s_nodes,
+                               const double* cash_div, const double* strike_call,
+                               int32_t* out_slots);
+
+/* Greeks epilogue: T trades, trade t of kind[t] reads readouts first[t] ..
+ * first[t]+k-1 (k per kind below) and writes out[t][FDCN_GK_NOUT] =
+ * price, delta, gamma, vega, theta, aux.  Readout r:
+ *   rint[r][FDCN_GK_NRINT] = slot, interp case (0: between ilo and ilo+1,
+ *                            1: V[0], 2: V[ilo]), ilo, idx, dg mode (0 none,
+ *                            1 three-point at idx, 2 cubic through idx-1..idx+2)
+ *   rdbl[r][FDCN_GK_NRDBL] = S_interp, s[ilo], s[ilo+1], S_dg, s[idx-1],
+ *                            s[idx], s[idx+1], s[idx+2]
+ * Node positions come from the host (bisection on its grids, as the pricers
+ * do); the formulas keep the reference's operation order.  Kinds, params:
+ *   FDCN_GK_BARRIER  2 readouts (base: interp + 3-point; sigma-bumped: interp)
+ *                    P = sigma, spot, carry, div_yield, r, dv   (…pricer.py:883-904)
+ *   FDCN_GK_CNLOG    3 readouts (base, sigma+dv, sigma-dv)
+ *                    P = sigma, S0, b, r, dv                    (…_cn.py:429-466)
+ *   FDCN_GK_AMERICAN 7 readouts (N and 2N: interp + cubic; sigma +h, -h, +2h,
+ *                    -2h at N; N_t = 2 num_space_nodes) P = sigma, spot, carry, r, h;
+ *                    aux = price_log2's Richardson       (fd_american_equity.py:925-1068)
+ *   FDCN_GK_READOUT  1 readout: price, delta, gamma of that vector */
+#define FDCN_GK_BARRIER 0
+#define FDCN_GK_CNLOG 1
+#define FDCN_GK_AMERICAN 2
+#define FDCN_GK_READOUT 3
+#define FDCN_GK_NPARAM 8
+#define FDCN_GK_NRINT 5
+#define FDCN_GK_NRDBL 8
+#define FDCN_GK_NOUT 6
+int fdcn_session_greeks(fdcn_session* s, int32_t T, const int32_t* kind, const int32_t* first,
+                        const double* tparams, int32_t R, const int32_t* rint,
+                        const double* rdbl, double* out);
+
+/* Copy n slots (each n_nodes long) back to out [n][n_nodes]. */
+int fdcn_session_fetch(fdcn_session* s, int32_t n, const int32_t* slots, int32_t n_nodes,
+                       double* out);
+
 /* ---- launch planning / introspection ---------------------------------- */
 /* Writes the kernel geometry a launch of B scenarios uses: waves per
  * scenario, nodes per lane, scenarios per workgroup, LDS bytes per workgroup,

@@ -1,0 +1,198 @@
+"""Device-resident sessions (csrc/fdcn_session.hip, session.py) on the MI355X.
+
+* a march in a session gives the host-array ABI's vectors bitwise (same
+  kernel); chained marches (v_init from slots) equal one long march;
+* the device dividend jump is bit-identical to fdcn_dividend_jump (the host C
+  restatement of fd_american_equity.py:479-553, :732-772, itself bitwise the
+  NumPy/reference spline);
+* the device Greeks epilogue equals the host epilogue of the facades on the
+  same GPU value vectors: bitwise for the barrier (…pricer.py:883-904) and
+  CN-log (_cn.py:429-466) kinds, whose formulas are plain arithmetic in the
+  reference's order; to 1e-9 relative (Delta/Gamma 1e-7) for the American
+  kind, whose 4x4 cubic fit is a different LU than numpy's LAPACK;
+* the American trades with one and two discrete dividends (device jumps)
+  match the reference's golden numbers (tolerances of test_gpu_pricers).
+"""
+import numpy as np
+import pytest
+
+from finite_difference_amd import capi, scenarios
+from finite_difference_amd.engine import Engine, HipBackend, group_solves, pack
+from finite_difference_amd.session import Session
+from plan_factory import random_solve
+
+pytestmark = pytest.mark.gpu
+
+
+class HipHostEpilogue:
+    """The HIP march with the value vectors copied back and the facades'
+    host epilogue (Engine.on_device is False for this backend)."""
+    name = "hip-host-epilogue"
+
+    def run_group(self, g):
+        return HipBackend().run_group(g)
+
+
+def host_engine():
+    return Engine(HipHostEpilogue())
+
+
+def test_session_march_and_fetch_equal_host_abi():
+    rng = np.random.default_rng(31)
+    solves = ([random_solve(rng, 2049, 64, 2, it=True) for _ in range(3)] +
+              [random_solve(rng, 1024, 80, 2, it=False) for _ in range(4)])
+    ref = Engine().run(solves)
+    with Session() as S:
+        slots = Engine().march_slots(S, solves)
+        assert S.slots() == len(solves)
+        for s, sl, r in zip(solves, slots, ref):
+            got = S.fetch([sl], s.n_nodes)[0]
+            assert np.array_equal(got, r)
+
+
+def test_chained_marches_equal_one_march():
+    """Two launches of n/2 steps, the second starting from the first's slots
+    (no Rannacher restart, tau0 carried), equal one n-step launch on the
+    IT path when tau is accumulated (tau mode 1 makes the split exact)."""
+    rng = np.random.default_rng(8)
+    n_time = 60
+    full = [random_solve(rng, 513, n_time, 2, it=True) for _ in range(3)]
+    for s in full:
+        s.tau_accumulate = True
+    ref = Engine().run(full)
+    import copy
+    first = [copy.copy(s) for s in full]
+    second = [copy.copy(s) for s in full]
+    for a, b in zip(first, second):
+        a.n_time = b.n_time = n_time // 2
+        b.n_ranna = 0
+        b.tau0 = capi.tau_sequence(a.tau0, a.dt, a.n_time)[-1]
+    with Session() as S:
+        e = Engine()
+        s1 = e.march_slots(S, first)
+        s2 = e.march_slots(S, second, list(s1))
+        got = S.fetch(s2, full[0].n_nodes)
+    # the split march restarts the IT multiplier at the segment boundary
+    # (lambda = 0 at every _solve_segment start, fd_american_equity.py:661),
+    # so compare with the oracle doing the same two segments
+    from backends import oracle_engine
+    o = oracle_engine()
+    mid = o.run(first)
+    for b, v in zip(second, mid):
+        b.v_init = v
+    want = o.run(second)
+    for g, w in zip(got, want):
+        assert np.max(np.abs(g - w)) <= 1e-10 * max(1.0, np.max(np.abs(w)))
+
+
+def test_device_dividend_jump_is_bitwise_host():
+    rng = np.random.default_rng(12)
+    n = 2049
+    B = 6
+    s = np.sort(rng.uniform(20.0, 400.0, (B, n)), axis=1)
+    v = np.maximum(160.0 - s, 0.0) + rng.uniform(0.0, 0.5, (B, n))
+    cash = rng.uniform(0.2, 4.0, B)
+    strike = np.where(np.arange(B) % 2 == 0, -1.0, 150.0)
+    ref = np.array([capi.dividend_jump(s[b], v[b], cash[b], strike[b]) for b in range(B)])
+    solves = []
+    for b in range(B):  # put the vectors into slots through a zero-step march
+        sv = random_solve(rng, n, 0, 0, it=False, ko=False)
+        sv.v_init = v[b].copy()
+        solves.append(sv)
+    with Session() as S:
+        sl = Engine().march_slots(S, solves)
+        assert np.array_equal(S.fetch(sl, n), v)
+        out = S.dividend_jump(sl, s, cash, strike)
+        got = S.fetch(out, n)
+    assert np.array_equal(got, ref)
+
+
+def test_session_rejects_bad_slots():
+    rng = np.random.default_rng(3)
+    sv = random_solve(rng, 300, 10, 2, it=False)
+    with Session() as S:
+        with pytest.raises(capi.FdcnError, match="slot"):
+            S.fetch([0], 300)
+        sl = Engine().march_slots(S, [sv])
+        with pytest.raises(capi.FdcnError, match="nodes"):
+            S.fetch(sl, 299)
+
+
+def _barrier_cases():
+    from conftest import load_golden
+    return load_golden("barrier_cases.json")["cases"]
+
+
+def test_barrier_device_epilogue_is_bitwise_host_epilogue():
+    from test_barrier_host import make
+    for case in _barrier_cases():
+        dev = make(case["inputs"], Engine())
+        host = make(case["inputs"], host_engine())
+        assert dev.price_log2() == host.price_log2(), case["name"]
+        assert dev.greeks_log2() == host.greeks_log2(), case["name"]
+
+
+def test_batched_runner_device_epilogue_is_bitwise_host():
+    from test_barrier_host import _mixed_rows
+    base = scenarios.runner_base_params("put", 64)
+    base.update(num_time_steps=40, grid_mode="explicit")
+    rows = _mixed_rows(25, 5)
+    a = scenarios.run_rows_batched(rows, base, Engine())
+    b = scenarios.run_rows_batched(rows, base, host_engine())
+    for ra, rb in zip(a, b):
+        for k in ("model_price", "model_delta", "model_gamma", "model_vega"):
+            assert ra[k] == rb[k] or (np.isnan(ra[k]) and np.isnan(rb[k])), (k, ra, rb)
+
+
+def test_cn_log_device_epilogue_is_bitwise_host():
+    import test_cn_log_host as T
+    from conftest import load_golden
+    for case in load_golden("cn_log_cases.json"):
+        inp = case["inputs"]
+        if not inp["bt"].endswith("out"):
+            continue
+        dev, host = T.make(inp, Engine()), T.make(inp, host_engine())
+        assert dev.price() == host.price()
+        assert dev.greeks() == host.greeks()
+
+
+@pytest.mark.parametrize("which", ["american", "black76"])
+def test_american_device_epilogue_matches_host(which):
+    if which == "american":
+        import test_american_host as T
+    else:
+        import test_black76_host as T
+    for case in T.CASES:
+        dev, host = T.make(case, Engine()), T.make(case, host_engine())
+        pd_, ph = dev.price_log2(), host.price_log2()
+        assert abs(pd_ - ph) <= 1e-12 * max(1.0, abs(ph)), (case["name"], pd_, ph)
+        gd, gh = dev.greeks_log2(), host.greeks_log2()
+        assert abs(gd["price"] - gh["price"]) <= 1e-12 * max(1.0, abs(gh["price"]))
+        assert abs(gd["vega"] - gh["vega"]) <= 1e-12 * max(1.0, abs(gh["vega"]))
+        for k in ("delta", "gamma", "theta"):
+            assert abs(gd[k] - gh[k]) <= 1e-7 * max(1.0, abs(gh[k])), (case["name"], k, gd, gh)
+
+
+def test_american_dividend_trades_on_device_match_reference():
+    """put_1div / call_2div: segments in lock-step launches, the spline jumps
+    on the device in between (no host round trip), Richardson epilogue on
+    the device; against the reference's own numbers."""
+    import test_american_host as T
+    from test_gpu_pricers import check_greeks, close
+    divs = [c for c in T.CASES if c["inputs"]["divs"]]
+    assert {c["name"] for c in divs} == {"put_1div", "call_2div"}
+    for case in divs:
+        p = T.make(case, Engine())
+        assert close("price", p.price_log2(), case["price_log2"])
+        check_greeks(p.greeks_log2(), case["greeks_log2"], "device " + case["name"])
+
+
+def test_prefetch_many_device_matches_single_trades():
+    import test_american_host as T
+    from finite_difference_amd.american import prefetch_many
+    batch = [T.make(c, Engine()) for c in T.CASES]
+    prefetch_many(batch)
+    for p, c in zip(batch, T.CASES):
+        one = T.make(c, Engine())
+        assert p.price_log2() == one.price_log2()
+        assert p.greeks_log2() == one.greeks_log2()
