@@ -38,7 +38,9 @@ EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batc
             "fdcn_abi_version", "fdcn_select_device", "fdcn_current_device",
             "fdcn_tau_sequence", "fdcn_tau_runs", "fdcn_session_create",
             "fdcn_session_destroy", "fdcn_session_slots", "fdcn_session_march",
-            "fdcn_session_dividend_jump", "fdcn_session_greeks", "fdcn_session_fetch")
+            "fdcn_session_dividend_jump", "fdcn_session_greeks", "fdcn_session_fetch",
+            "fdcn_vc_batch", "fdcn_vc_batch_dev", "fdcn_vc_plan")
+VC_NDIAG = 6
 RR_NPARAM, RR_NFLAG = 8, 5
 DB_NPARAM, DB_NFLAG = 8, 3
 
@@ -124,6 +126,13 @@ def lib() -> ctypes.CDLL:
             L.fdcn_tau_sequence.argtypes = [ctypes.c_double, ctypes.c_double, _I, _V]
             L.fdcn_tau_runs.restype = _I
             L.fdcn_tau_runs.argtypes = [ctypes.c_double, ctypes.c_double, _I]
+            L.fdcn_vc_batch.restype = _I
+            L.fdcn_vc_batch.argtypes = [_I, _I, _I, _I, _V, _V, _V, _V, _I, _V, _V, _V]
+            L.fdcn_vc_batch_dev.restype = _I
+            L.fdcn_vc_batch_dev.argtypes = [_I, _I, _I, _I, _V, _V, _V, _V, _I, _V, _V, _V, _V,
+                                            _I64, _V]
+            L.fdcn_vc_plan.restype = _I
+            L.fdcn_vc_plan.argtypes = [_I, _I, _PI, _PI, ctypes.POINTER(ctypes.c_int64)]
             L.fdcn_select_device.restype = ctypes.c_int
             L.fdcn_select_device.argtypes = [_I]
             L.fdcn_current_device.restype = ctypes.c_int
@@ -237,6 +246,29 @@ def it_batch_dev(B: int, n_nodes: int, n_time: int, n_ranna: int, params_ptr: in
     _check(lib().fdcn_it_batch_dev(B, n_nodes, n_time, n_ranna, params_ptr, iparams_ptr,
                                    v_init_ptr, payoff_ptr, v_out_ptr, k_cap, workspace_ptr,
                                    workspace_bytes, stream_ptr))
+
+
+def vc_batch(n_nodes: int, n_time: int, n_ranna: int, diag, bnd, v_init, iparams, mon_step,
+             mon_rebate) -> np.ndarray:
+    """Spot-space CN with per-row coefficients (fdcn_vc_batch) -> v_out [B, n_nodes].
+    diag [B, 2, VC_NDIAG, n_nodes], bnd [B, n_time, 2]."""
+    require_device()
+    D, Bd, V, I = _f64(diag), _f64(bnd), _f64(v_init), _i32(iparams)
+    B = V.shape[0]
+    ms = _i32(mon_step if len(mon_step) else [0])
+    mr = _f64(mon_rebate if len(mon_rebate) else [0.0])
+    out = np.empty((B, n_nodes), dtype=np.float64)
+    _check(lib().fdcn_vc_batch(B, n_nodes, n_time, n_ranna, D.ctypes.data, Bd.ctypes.data,
+                               V.ctypes.data, I.ctypes.data, len(mon_step), ms.ctypes.data,
+                               mr.ctypes.data, out.ctypes.data))
+    return out
+
+
+def vc_plan(n_nodes: int, *, B: int) -> dict:
+    w, npt = ctypes.c_int32(), ctypes.c_int32()
+    ws = ctypes.c_int64()
+    _check(lib().fdcn_vc_plan(B, n_nodes, ctypes.byref(w), ctypes.byref(npt), ctypes.byref(ws)))
+    return dict(waves=w.value, npt=npt.value, ws_bytes_per_scen=ws.value)
 
 
 def log_grid(x_min: float, dx: float, n: int):

@@ -157,10 +157,80 @@ def group_solves(solves: Sequence[Solve]) -> List[Group]:
     return [pack([solves[i] for i in idx], idx) for idx in buckets.values()]
 
 
+@dataclass
+class VcSolve:
+    """One spot-space march with per-row coefficients (fdcn_vc_batch):
+    diag [2, 6, n] = sub, main, sup, a, b, c of the implicit / explicit
+    matrices for the Rannacher phase and the Crank-Nicolson phase; bnd
+    [n_time, 2] = the Dirichlet values of rows 0 and n-1 per step."""
+    n_time: int
+    n_ranna: int
+    diag: np.ndarray
+    bnd: np.ndarray
+    v_init: np.ndarray
+    ko_lo: int = -1
+    ko_hi: int = 1 << 30
+    mon_steps: Sequence[int] = ()
+    mon_rebates: Sequence[float] = ()
+
+    @property
+    def n_nodes(self) -> int:
+        return int(self.v_init.shape[0])
+
+    def key(self) -> Tuple[int, int, int]:
+        return (self.n_nodes, int(self.n_time), int(self.n_ranna))
+
+
+@dataclass
+class VcGroup:
+    n_nodes: int
+    n_time: int
+    n_ranna: int
+    diag: np.ndarray      # [B, 2, 6, n]
+    bnd: np.ndarray       # [B, n_time, 2]
+    v_init: np.ndarray
+    iparams: np.ndarray
+    mon_step: np.ndarray
+    mon_rebate: np.ndarray
+    index: List[int] = field(default_factory=list)
+
+    @property
+    def B(self) -> int:
+        return int(self.v_init.shape[0])
+
+
+def pack_vc(solves: Sequence[VcSolve], index: Sequence[int]) -> VcGroup:
+    s0 = solves[0]
+    B, n = len(solves), s0.n_nodes
+    I = np.zeros((B, NIPARAM), dtype=np.int32)
+    mstep: List[int] = []
+    mreb: List[float] = []
+    for i, s in enumerate(solves):
+        if s.key() != s0.key():
+            raise ValueError("solves in one group must share (n_nodes, n_time, n_ranna)")
+        I[i, capi.I_KO_LO] = max(-1, min(int(s.ko_lo), n))
+        I[i, capi.I_KO_HI] = max(-1, min(int(s.ko_hi), n + 1))
+        if len(s.mon_steps):
+            I[i, capi.I_MON_START] = len(mstep)
+            I[i, capi.I_MON_COUNT] = len(s.mon_steps)
+            mstep.extend(int(k) for k in s.mon_steps)
+            mreb.extend(float(x) for x in s.mon_rebates)
+    return VcGroup(n, int(s0.n_time), int(s0.n_ranna),
+                   np.ascontiguousarray(np.stack([s.diag for s in solves]), dtype=np.float64),
+                   np.ascontiguousarray(np.stack([np.asarray(s.bnd, np.float64).reshape(-1, 2)
+                                                  for s in solves])),
+                   np.ascontiguousarray(np.stack([s.v_init for s in solves]), dtype=np.float64),
+                   I, np.asarray(mstep, np.int32), np.asarray(mreb, np.float64), list(index))
+
+
 class HipBackend:
     """Runs a packed group on the MI355X through libfdcn (host-pointer ABI)."""
 
     name = "hip"
+
+    def run_vc_group(self, g: VcGroup) -> np.ndarray:
+        return capi.vc_batch(g.n_nodes, g.n_time, g.n_ranna, g.diag, g.bnd, g.v_init,
+                             g.iparams, g.mon_step, g.mon_rebate)
 
     def run_group(self, g: Group) -> np.ndarray:
         if g.it:
@@ -217,6 +287,21 @@ class Engine:
             self.launches += 1
             self.solves += g.B
         return out
+
+    def run_vc(self, solves: Sequence[VcSolve]) -> List[np.ndarray]:
+        """Spot-space per-row-coefficient marches, one launch per shape."""
+        buckets: Dict[Tuple, List[int]] = {}
+        for i, s in enumerate(solves):
+            buckets.setdefault(s.key(), []).append(i)
+        out: List[Optional[np.ndarray]] = [None] * len(solves)
+        for idx in buckets.values():
+            g = pack_vc([solves[i] for i in idx], idx)
+            res = self.backend.run_vc_group(g)
+            self.launches += 1
+            self.solves += g.B
+            for row, i in enumerate(g.index):
+                out[i] = res[row]
+        return out  # type: ignore[return-value]
 
     def run(self, solves: Sequence[Solve]) -> List[np.ndarray]:
         out: List[Optional[np.ndarray]] = [None] * len(solves)

@@ -240,6 +240,39 @@ int fdcn_plan(int32_t B, int32_t n_nodes, int32_t n_time, int32_t it_mode, int32
 int fdcn_sm_extent(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                    const double* params);
 
+/* ---- spot-space CN with per-row coefficients ---------------------------
+ * fdcn_vc_batch <- DiscreteBarrierFDMPricer2._solve_pde_backward
+ *                    (discrete_barrier_fdm_pricer_2.py:336-428, FIS barrier
+ *                    rows and BGK window) and
+ *                  DiscreteBarrierFDMPricerAnalytic._cn_stepper
+ *                    (discrete_barrier_analytic_pricer.py:384-432).
+ * The matrices are tridiagonal with a different row at every node (uniform S
+ * grid, sigma^2 S_i^2 terms, the non-symmetric rows at the barrier), constant
+ * in time within a phase: phase 0 for steps m < n_ranna (Rannacher), phase 1
+ * after.  Step m: rhs_i = a_i V_{i-1} + b_i V_i + c_i V_{i+1} for interior
+ * rows, rhs_0 = bnd[m][0], rhs_{n-1} = bnd[m][1]; solve
+ * sub_i x_{i-1} + main_i x_i + sup_i x_{i+1} = rhs_i (sub_0 = sup_{n-1} = 0);
+ * V = x; then the knock-out projection of the CN ABI (iparams KO_LO / KO_HI,
+ * MON_START / MON_COUNT; LO/HI_FORM and TAU_MODE unused, pass 0).
+ *   diag [B][2][FDCN_VC_NDIAG][n_nodes]  sub, main, sup, a, b, c per phase
+ *   bnd  [B][n_time][2]                  Dirichlet values of rows 0 / n-1
+ * The LU factors of each phase are computed once per launch; the march
+ * keeps the rows' factored coefficients and V in registers. */
+#define FDCN_VC_NDIAG 6
+int fdcn_vc_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                  const double* diag, const double* bnd, const double* v_init,
+                  const int32_t* iparams, int32_t n_mon, const int32_t* mon_step,
+                  const double* mon_rebate, double* v_out);
+int fdcn_vc_batch_dev(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                      const double* diag, const double* bnd, const double* v_init,
+                      const int32_t* iparams, int32_t n_mon, const int32_t* mon_step,
+                      const double* mon_rebate, double* v_out, double* workspace,
+                      int64_t workspace_bytes, void* stream);
+/* geometry of a fdcn_vc launch of B scenarios (depends on B): waves per
+ * scenario, nodes per lane, device workspace per scenario (bytes) */
+int fdcn_vc_plan(int32_t B, int32_t n_nodes, int32_t* waves, int32_t* npt,
+                 int64_t* ws_bytes_per_scen);
+
 /* ---- batched closed-form barrier engines (one thread per contract) ------ */
 /* Reiner-Rubinstein single continuous barrier with cash rebate and barrier
  * status; replaces BarrierEngine(s,b,r,t,x,sigma,h,optionflag,directionflag,

@@ -393,6 +393,91 @@ int oracle_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
                     NULL, v_out, nthreads);
 }
 
+/* ---------------------------------------------------------------------- */
+/* 3. spot-space CN with per-row coefficients                             */
+/*    DiscreteBarrierFDMPricer2._solve_pde_backward                       */
+/*      (discrete_barrier_fdm_pricer_2.py:336-428) and                    */
+/*    DiscreteBarrierFDMPricerAnalytic._cn_stepper                        */
+/*      (discrete_barrier_analytic_pricer.py:384-432), on the plan arrays */
+/*    of fdcn_vc_batch: per scenario and phase (0: the Rannacher steps,   */
+/*    1: the rest) the rows' sub/main/sup of the implicit matrix and the  */
+/*    explicit a/b/c coefficients; rows 0 and n-1 take the per-step       */
+/*    Dirichlet values as their rhs.  Thomas as _solve_tridiagonal        */
+/*    (:273-297).                                                         */
+/* ---------------------------------------------------------------------- */
+static void vc_solve_one(int n, int n_time, int n_ranna, const double* D, const double* bnd,
+                         const double* v_init, const int32_t* I, const int32_t* mon_step,
+                         const double* mon_rebate, double* v_out, double* work) {
+  double* V = work;
+  double* rhs = V + n;
+  double* cs = rhs + n;
+  double* ds = cs + n;
+  double* x = ds + n;
+  memcpy(V, v_init, sizeof(double) * (size_t)n);
+  int mon_pos = I[FDCN_I_MON_START];
+  const int mon_end = mon_pos + I[FDCN_I_MON_COUNT];
+  const int ko_lo = I[FDCN_I_KO_LO], ko_hi = I[FDCN_I_KO_HI];
+  for (int m = 0; m < n_time; ++m) {
+    const double* P = D + (size_t)(m < n_ranna ? 0 : 1) * FDCN_VC_NDIAG * n;
+    const double *sub = P, *main_ = P + n, *sup = P + 2 * n;
+    const double *ae = P + 3 * n, *be = P + 4 * n, *ce = P + 5 * n;
+    rhs[0] = bnd[2 * (size_t)m];
+    rhs[n - 1] = bnd[2 * (size_t)m + 1];
+    for (int i = 1; i < n - 1; ++i) rhs[i] = ae[i] * V[i - 1] + be[i] * V[i] + ce[i] * V[i + 1];
+    double beta = main_[0];
+    cs[0] = sup[0] / beta;
+    ds[0] = rhs[0] / beta;
+    for (int i = 1; i < n; ++i) {
+      beta = main_[i] - sub[i] * cs[i - 1];
+      cs[i] = (i < n - 1) ? sup[i] / beta : 0.0;
+      ds[i] = (rhs[i] - sub[i] * ds[i - 1]) / beta;
+    }
+    x[n - 1] = ds[n - 1];
+    for (int i = n - 2; i >= 0; --i) x[i] = ds[i] - cs[i] * x[i + 1];
+    memcpy(V, x, sizeof(double) * (size_t)n);
+    if (mon_pos < mon_end && mon_step[mon_pos] == m + 1) {
+      const double reb = mon_rebate[mon_pos];
+      for (int j = 0; j < n; ++j)
+        if (j <= ko_lo || j >= ko_hi) V[j] = reb;
+      ++mon_pos;
+    }
+    while (mon_pos < mon_end && mon_step[mon_pos] <= m + 1) ++mon_pos;
+  }
+  memcpy(v_out, V, sizeof(double) * (size_t)n);
+}
+
+int oracle_vc_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                    const double* diag, const double* bnd, const double* v_init,
+                    const int32_t* iparams, int32_t n_mon, const int32_t* mon_step,
+                    const double* mon_rebate, double* v_out, int32_t nthreads) {
+  (void)n_mon;
+  if (B < 0 || n_nodes < 3 || n_time < 0) return FDCN_EINVAL;
+  int err = 0;
+#ifdef _OPENMP
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+  {
+    double* work = (double*)malloc(sizeof(double) * 5 * (size_t)n_nodes);
+    if (!work) {
+      err = FDCN_ENOMEM;
+    } else {
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+      for (int32_t b = 0; b < B; ++b)
+        vc_solve_one(n_nodes, n_time, n_ranna,
+                     diag + (size_t)b * 2 * FDCN_VC_NDIAG * n_nodes,
+                     bnd + (size_t)b * 2 * (size_t)n_time,
+                     v_init + (size_t)b * n_nodes, iparams + (size_t)b * FDCN_NIPARAM,
+                     mon_step, mon_rebate, v_out + (size_t)b * n_nodes, work);
+      free(work);
+    }
+  }
+  (void)nthreads;
+  return err;
+}
+
 int oracle_max_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

@@ -62,6 +62,9 @@ def lib() -> ctypes.CDLL:
                                       _PD, _I32]
         L.oracle_it_batch.restype = _I
         L.oracle_it_batch.argtypes = [_I32, _I32, _I32, _I32, _PD, _PI32, _PD, _PD, _PD, _I32]
+        L.oracle_vc_batch.restype = _I
+        L.oracle_vc_batch.argtypes = [_I32, _I32, _I32, _I32, _PD, _PD, _PD, _PI32, _I32, _PI32,
+                                      _PD, _PD, _I32]
         L.oracle_max_threads.restype = _I
         _lib = L
     return _lib
@@ -171,6 +174,25 @@ def it_batch(n_nodes: int, n_time: int, n_ranna: int, params, iparams, v_init, p
                                _pd(V), _pd(F), _pd(out), int(nthreads))
     if rc != 0:
         raise RuntimeError(f"oracle_it_batch failed ({rc})")
+    return out
+
+
+def vc_batch(n_nodes: int, n_time: int, n_ranna: int, diag, bnd, v_init, iparams, mon_step,
+             mon_rebate, nthreads: int = 1) -> np.ndarray:
+    """Spot-space CN with per-row coefficients on the fdcn_vc_batch plan
+    (discrete_barrier_fdm_pricer_2.py:336-428): sequential Thomas per step."""
+    D, Bd, V, I = _f64(diag), _f64(bnd), _f64(v_init), _i32(iparams)
+    B = V.shape[0]
+    ms = _i32(mon_step) if len(mon_step) else _i32([0])
+    mr = _f64(mon_rebate) if len(mon_rebate) else _f64([0.0])
+    if Bd.size == 0:
+        Bd = _f64([0.0, 0.0])
+    out = np.empty((B, n_nodes), dtype=np.float64)
+    rc = lib().oracle_vc_batch(B, n_nodes, n_time, n_ranna, _pd(D), _pd(Bd), _pd(V),
+                               I.ctypes.data_as(_PI32), len(mon_step), ms.ctypes.data_as(_PI32),
+                               _pd(mr), _pd(out), int(nthreads))
+    if rc != 0:
+        raise RuntimeError(f"oracle_vc_batch failed ({rc})")
     return out
 
 

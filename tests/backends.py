@@ -22,6 +22,11 @@ class OracleBackend:
         return oracle.cn_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams, g.v_init,
                                g.mon_step, g.mon_rebate, self.nthreads)
 
+    def run_vc_group(self, g):
+        from oracle import oracle
+        return oracle.vc_batch(g.n_nodes, g.n_time, g.n_ranna, g.diag, g.bnd, g.v_init,
+                               g.iparams, g.mon_step, g.mon_rebate, self.nthreads)
+
 
 def oracle_engine() -> Engine:
     return Engine(OracleBackend())

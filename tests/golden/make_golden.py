@@ -334,6 +334,51 @@ def gen_double_out():
     dump("double_out_cases.json", dict(cases=cases))
 
 
+def gen_spot():
+    """DiscreteBarrierFDMPricer2 (discrete_barrier_fdm_pricer_2.py): the
+    spot-space CN with per-row coefficients, the FIS barrier rows and the BGK
+    window.  Its explicit off-diagonals have the wrong sign (:383-385), so the
+    prices grow without bound with M; at the small step counts below they are
+    still finite, and the value vectors pin the march to the reference."""
+    sys.path.insert(0, REF)
+    import discrete_barrier_fdm_pricer_2 as m  # type: ignore
+    v0, v1 = dt.date(2025, 7, 28), dt.date(2026, 1, 28)
+    daily = [v0 + dt.timedelta(days=i) for i in range(1, 40)]
+    weekly = [v0 + dt.timedelta(days=7 * i) for i in range(1, 27)]
+    specs = [
+        dict(name="vanilla_call", spot=100.0, strike=100.0, volatility=0.25, option_type="call",
+             barrier_type="none", flat_rate_nacc=0.05, num_space_nodes=200, num_time_steps=6),
+        dict(name="put_do_weekly", spot=100.0, strike=105.0, volatility=0.3, option_type="put",
+             barrier_type="down-and-out", lower_barrier=85.0, monitoring_dates=weekly,
+             flat_rate_nacc=0.04, num_space_nodes=220, num_time_steps=8),
+        dict(name="call_uo_weekly", spot=100.0, strike=95.0, volatility=0.22, option_type="call",
+             barrier_type="up-and-out", upper_barrier=125.0, monitoring_dates=weekly,
+             flat_rate_nacc=0.05, num_space_nodes=200, num_time_steps=5),
+        dict(name="dko_bgk_window", spot=100.0, strike=100.0, volatility=0.2, option_type="call",
+             barrier_type="double-out", lower_barrier=80.0, upper_barrier=130.0,
+             monitoring_dates=daily, flat_rate_nacc=0.05, num_space_nodes=200, num_time_steps=3),
+        dict(name="put_di_divs", spot=100.0, strike=100.0, volatility=0.25, option_type="put",
+             barrier_type="down-and-in", lower_barrier=90.0, monitoring_dates=weekly,
+             flat_rate_nacc=0.05, dividends=[(dt.date(2025, 10, 15), 1.5)],
+             num_space_nodes=200, num_time_steps=4),
+    ]
+    cases = []
+    for sp in specs:
+        kw = dict(sp)
+        name = kw.pop("name")
+        p = m.DiscreteBarrierFDMPricer2(valuation_date=v0, maturity_date=v1, **kw)
+        Sg, Vg, S_eff = p._solve_grid_once()
+        rec = dict(name=name, inputs={k: ([[iso(a), b] for a, b in v] if k == "dividends" else
+                                         ([iso(d) for d in v] if k == "monitoring_dates" else v))
+                                     for k, v in sp.items()},
+                   S_shifted=Sg, V=Vg, S_eff=S_eff, price=p.price(), greeks=p.greeks(),
+                   use_bgk=p.use_bgk_correction, bgk=[p.bgk_lower, p.bgk_upper],
+                   window=[p.k_first_cont, p.k_last_cont],
+                   monitor_map=sorted(p._monitoring_step_map()), S_nodes=p.S_nodes)
+        cases.append(rec)
+    dump("spot_cases.json", dict(valuation=iso(v0), maturity=iso(v1), cases=cases))
+
+
 # --------------------------------------------------------------------------
 # 3. American engine
 # --------------------------------------------------------------------------
@@ -473,7 +518,8 @@ def gen_analytic():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["cn", "barrier", "double", "american", "analytic", "black76"]
+    which = sys.argv[1:] or ["cn", "barrier", "double", "spot", "american", "analytic",
+                             "black76"]
     if "black76" in which:
         gen_black76()
     if "cn" in which:
@@ -482,6 +528,8 @@ if __name__ == "__main__":
         gen_barrier()
     if "double" in which:
         gen_double_out()
+    if "spot" in which:
+        gen_spot()
     if "american" in which:
         gen_american(with_config2="config2" in which or not sys.argv[1:])
     if "analytic" in which:
