@@ -149,8 +149,15 @@ def _check(rc: int) -> None:
         raise FdcnError(f"fdcn error {rc}: {msg}")
 
 
+_n_devices: Optional[int] = None
+
+
 def device_count() -> int:
-    return int(lib().fdcn_device_count())
+    """gfx950 devices visible (queried once per process)."""
+    global _n_devices
+    if _n_devices is None:
+        _n_devices = int(lib().fdcn_device_count())
+    return _n_devices
 
 
 def require_device() -> None:

@@ -327,8 +327,12 @@ struct KArgs {
   int n_pad;        // n_time rounded up to a multiple of 64
 };
 
-// ZG: the Sherman-Morrison table lives in the global workspace instead of
-// LDS -- the fallback for correction extents too long for LDS (|fm| -> 1).
+// ZG is a flag set.  Bit 0: the Sherman-Morrison table lives in the global
+// workspace instead of LDS -- the fallback for correction extents too long
+// for LDS (|fm| -> 1).  Bit 1: the single-trade flavour of a W = 1 variant,
+// for batches too small to put a wave on every SIMD: its recurrences run as 4
+// interleaved sub-chains per lane, trading the joins' extra FMAs for in-wave
+// ILP (with one wave on a SIMD nothing else hides the FMA latency).
 template <int IT, int W, int NPT, int ZG = 0>
 struct Geo {
   static constexpr int L = 64 * W;
@@ -341,7 +345,7 @@ struct Geo {
 // doubles of LDS per scenario
 template <int IT, int W, int NPT, int ZG = 0>
 __host__ __device__ inline int lds_doubles_per_scen(int lz) {
-  return (ZG ? 0 : 2 * lz * (NPT + 1)) + (Geo<IT, W, NPT, ZG>::kPhiLds ? 64 * W * NPT : 0) +
+  return ((ZG & 1) ? 0 : 2 * lz * (NPT + 1)) + (Geo<IT, W, NPT, ZG>::kPhiLds ? 64 * W * NPT : 0) +
          (W > 1 ? Xch<W>::kSize : 0);
 }
 
@@ -379,8 +383,8 @@ fdcn_march(KArgs A) {
   constexpr bool kPhiLds = Geo<IT, W, NPT, ZG>::kPhiLds;
   double* my = lds + (size_t)scen_in_blk * lds_doubles_per_scen<IT, W, NPT, ZG>(lz);
   // SM table [2][lz][NPT+1]: LDS, or this scenario's workspace slice (ZG)
-  double* ztab = ZG ? A.zg + (size_t)scen * 2 * lz * (NPT + 1) : my;
-  double* phit = my + (ZG ? 0 : 2 * lz * (NPT + 1));  // payoff [NPT][L] (kPhiLds)
+  double* ztab = (ZG & 1) ? A.zg + (size_t)scen * 2 * lz * (NPT + 1) : my;
+  double* phit = my + ((ZG & 1) ? 0 : 2 * lz * (NPT + 1));  // payoff [NPT][L] (kPhiLds)
   double* xch = phit + (kPhiLds ? L * NPT : 0);       // exchange area (W > 1)
   (void)xch;
 
@@ -478,8 +482,9 @@ fdcn_march(KArgs A) {
   // 2 12.31 -> 12.08 ms, config 3 6.54 -> 6.21 ms, config 5 20.65 -> 19.69 ms
   // against S = 4).  The multi-wave variants serve small batches, where one
   // wave per SIMD needs the in-wave ILP: they keep 4.
-  constexpr int S = (W == 1) ? (NPT >= 48 ? 2 : 1)
-                             : ((NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1));
+  constexpr int S = (W == 1 && !(ZG & 2))
+                        ? (NPT >= 48 ? 2 : 1)
+                        : ((NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1));
   constexpr int M = NPT / S;
 
   // ---- per-theta constants: scan window products + SM table -------------
@@ -1423,12 +1428,13 @@ struct Variant {
   int threads, spb;
   int (*lds_per_scen)(int lz);  // the kernel's own LDS layout, in doubles
   int zg;                       // correction table in the workspace
+  int lat;                      // single-trade (in-wave ILP) flavour
 };
 
 template <int IT, int W, int NPT, int ZG = 0>
 Variant mk() {
   return Variant{IT, W, NPT, &fdcn_march<IT, W, NPT, ZG>, Geo<IT, W, NPT, ZG>::kThreads,
-                 Geo<IT, W, NPT, ZG>::SPB, &lds_doubles_per_scen<IT, W, NPT, ZG>, ZG};
+                 Geo<IT, W, NPT, ZG>::SPB, &lds_doubles_per_scen<IT, W, NPT, ZG>, ZG & 1, ZG >> 1};
 }
 
 // W=1: throughput (one wavefront per scenario).  W>1: grids beyond 64*64
@@ -1440,7 +1446,8 @@ Variant mk() {
       mk<IT, 2, 32>(), mk<IT, 2, 40>(), mk<IT, 4, 8>(), mk<IT, 4, 16>(), mk<IT, 4, 24>(),   \
       mk<IT, 4, 40>(), mk<IT, 8, 8>(), mk<IT, 8, 16>(), mk<IT, 8, 40>(), mk<IT, 16, 8>(),   \
       mk<IT, 16, 24>(), mk<IT, 16, 40>(), mk<IT, 1, 64, 1>(), mk<IT, 4, 40, 1>(),           \
-      mk<IT, 8, 40, 1>(), mk<IT, 16, 40, 1>()
+      mk<IT, 8, 40, 1>(), mk<IT, 16, 40, 1>(), mk<IT, 1, 8, 2>(), mk<IT, 1, 16, 2>(),       \
+      mk<IT, 1, 32, 2>()
 
 const Variant kVariants[] = {FDCN_VARIANTS(0), FDCN_VARIANTS(1)};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
@@ -1482,13 +1489,14 @@ constexpr long kResidentWaves = 2048;
 const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
   const int n_int = n_nodes - 2;
   if (n_int < 3) return nullptr;
-  if (const char* f = getenv("FDCN_VARIANT")) {
-    int w = 0, npt = 0;
-    if (sscanf(f, "%d,%d", &w, &npt) == 2)
+  if (const char* f = getenv("FDCN_VARIANT")) {  // "W,NPT" or "W,NPT,L" (L=1: single-trade)
+    int w = 0, npt = 0, lat = 0;
+    if (sscanf(f, "%d,%d,%d", &w, &npt, &lat) >= 2)
       for (int zg = 0; zg < 2; ++zg)
         for (int i = 0; i < kNumVariants; ++i)
           if (kVariants[i].it == it && kVariants[i].w == w && kVariants[i].npt == npt &&
-              kVariants[i].zg == zg && fits(kVariants[i], n_int, k_cap, zg == 0))
+              kVariants[i].zg == zg && kVariants[i].lat == lat &&
+              fits(kVariants[i], n_int, k_cap, zg == 0))
             return &kVariants[i];
   }
   const Variant* best = nullptr;
@@ -1500,7 +1508,8 @@ const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
   for (int pass = 0; pass < 3 && !best; ++pass) {
     for (int i = 0; i < kNumVariants; ++i) {
       const Variant& v = kVariants[i];
-      if (v.it != it || v.zg != (pass == 2) || !fits(v, n_int, k_cap, pass == 0)) continue;
+      if (v.it != it || v.lat || v.zg != (pass == 2) || !fits(v, n_int, k_cap, pass == 0))
+        continue;
       const long slots = (long)64 * v.w * v.npt;
       if (!best || v.w < best_w || (v.w == best_w && slots < best_slots)) {
         best = &v;
@@ -1509,14 +1518,25 @@ const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
       }
     }
   }
-  // Small batch of long chunks: the measured win is splitting 48-64-node
-  // chunks to ~16 across waves (config 5, one 4096-node solve: 17.1 -> 12.8
-  // ms); shorter chunks lose it again to the per-step barriers.
+  // Batches too small to put a wave on every SIMD: the single-trade flavour
+  // of the chosen W = 1 variant (in-wave ILP), compiled for NPT 8-32.
+  // Measured on one trade (bench.py trade_*): config-2 grids 8.42 -> 8.28 ms,
+  // config 1 unchanged; for 64-node chunks (config 5) the split over 4 waves
+  // below wins (12.0 ms against 13.5 for either W = 1 flavour).
+  if (best && best->w == 1 && best->npt < 48 && B * best->w <= kResidentWaves / 2 && !best->zg)
+    for (int i = 0; i < kNumVariants; ++i) {
+      const Variant& v = kVariants[i];
+      if (v.lat && v.it == it && v.w == 1 && v.npt == best->npt && !v.zg) return &v;
+    }
+  // Small batch of long chunks without a single-trade flavour: split 48-64-
+  // node chunks to ~16 across waves (config 5, one 4096-node solve: 17.1 ->
+  // 12.8 ms); shorter chunks lose it again to the per-step barriers.
   if (!best || best->npt < 48 || B * best->w >= kResidentWaves / 2) return best;
   const Variant* lat = best;
   for (int i = 0; i < kNumVariants; ++i) {
     const Variant& v = kVariants[i];
-    if (v.it != it || v.zg || !fits(v, n_int, k_cap) || v.npt < 16 || B * v.w > kResidentWaves)
+    if (v.it != it || v.zg || v.lat || !fits(v, n_int, k_cap) || v.npt < 16 ||
+        B * v.w > kResidentWaves)
       continue;
     if (v.npt < lat->npt || (v.npt == lat->npt && v.w < lat->w)) lat = &v;
   }

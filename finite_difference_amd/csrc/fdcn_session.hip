@@ -310,37 +310,55 @@ int readouts_per_kind(int kind) {
   }
 }
 
-// session-lifetime pinned staging (every async copy reads/writes a region no
-// later call reuses; released by fdcn_session_destroy)
+// Pinned staging: within a session every async copy reads/writes a region no
+// later call of that session reuses; the regions are recycled only after
+// fdcn_session_destroy has synchronised the session's streams.
 struct PinnedArena {
-  std::vector<char*> chunks;
-  size_t used = 0, cap = 0;
+  struct Chunk {
+    char* p;
+    size_t cap;
+  };
+  std::vector<Chunk> chunks;
+  size_t cur = 0, used = 0;
   char* get(size_t bytes) {
     bytes = al256(bytes > 0 ? bytes : 1);
-    if (chunks.empty() || used + bytes > cap) {
+    while (cur < chunks.size() && used + bytes > chunks[cur].cap) {
+      ++cur;
+      used = 0;
+    }
+    if (cur == chunks.size()) {
       const size_t sz = std::max(bytes, (size_t)8 << 20);
       char* p = nullptr;
       if (hipHostMalloc((void**)&p, sz, hipHostMallocDefault) != hipSuccess) return nullptr;
-      chunks.push_back(p);
+      chunks.push_back({p, sz});
       used = 0;
-      cap = sz;
     }
-    char* r = chunks.back() + used;
+    char* r = chunks[cur].p + used;
     used += bytes;
     return r;
   }
-  void release() {
-    for (char* p : chunks) (void)hipHostFree(p);
-    chunks.clear();
-    used = cap = 0;
-  }
+  void reset() { cur = used = 0; }
 };
+
+// Per-thread, per-device resources a session borrows: streams, spare events
+// and the pinned arena.  Creating them costs far more than a small trade's
+// march (streams ~100 us, an 8 MB pinned chunk ~1 ms), so fdcn_session_destroy
+// hands them back to the thread's idle list instead of releasing them
+// (they live until the process ends).
+struct Ctx {
+  int device = 0;
+  std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> spare_events;
+  PinnedArena pinned;
+};
+thread_local std::vector<Ctx*> t_idle_ctx;
 
 }  // namespace
 
 struct fdcn_session {
   int device = 0;
-  std::vector<hipStream_t> streams;
+  Ctx* ctx = nullptr;
+  std::vector<hipStream_t> streams;  // the ctx streams this session has used
   int rr = 0;
   std::vector<hipEvent_t> events;
   std::vector<double*> slot_ptr;
@@ -351,15 +369,20 @@ struct fdcn_session {
     hipStream_t s;
   };
   std::vector<Block> blocks;
-  PinnedArena pinned;
+  PinnedArena& pinned() { return ctx->pinned; }
 };
 
 namespace {
 
 int pick_stream(fdcn_session* s, hipStream_t* out) {
   if ((int)s->streams.size() < kMaxStreams) {
-    hipStream_t st;
-    S_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    Ctx* c = s->ctx;
+    if (c->streams.size() <= s->streams.size()) {
+      hipStream_t st;
+      S_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      c->streams.push_back(st);
+    }
+    hipStream_t st = c->streams[s->streams.size()];
     s->streams.push_back(st);
     *out = st;
     return FDCN_OK;
@@ -402,7 +425,12 @@ int alloc_block(fdcn_session* s, hipStream_t st, size_t bytes, char** out) {
 // record the completion of the work just queued on `st`; returns the event id
 int record(fdcn_session* s, hipStream_t st, int32_t* ev) {
   hipEvent_t e;
-  S_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (!s->ctx->spare_events.empty()) {
+    e = s->ctx->spare_events.back();
+    s->ctx->spare_events.pop_back();
+  } else {
+    S_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   S_TRY(hipEventRecord(e, st));
   s->events.push_back(e);
   *ev = (int32_t)s->events.size() - 1;
@@ -430,16 +458,27 @@ int fdcn_session_create(fdcn_session** out) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
     return sfail(FDCN_ENODEV, "no HIP device visible");
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return sfail(FDCN_EHIP, "hipGetDevice failed");
+  Ctx* c = nullptr;
+  for (size_t i = 0; i < t_idle_ctx.size(); ++i)
+    if (t_idle_ctx[i]->device == dev) {
+      c = t_idle_ctx[i];
+      t_idle_ctx.erase(t_idle_ctx.begin() + (long)i);
+      break;
+    }
+  if (!c) {
+    c = new Ctx();
+    c->device = dev;
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;  // keep freed blocks in the pool between sessions
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
   fdcn_session* s = new fdcn_session();
-  if (hipGetDevice(&s->device) != hipSuccess) {
-    delete s;
-    return sfail(FDCN_EHIP, "hipGetDevice failed");
-  }
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, s->device) == hipSuccess) {
-    uint64_t keep = UINT64_MAX;  // keep freed blocks in the pool between sessions
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-  }
+  s->device = dev;
+  s->ctx = c;
   *out = s;
   return FDCN_OK;
 }
@@ -452,12 +491,13 @@ int fdcn_session_destroy(fdcn_session* s) {
   if (cur != s->device) (void)hipSetDevice(s->device);
   for (auto& b : s->blocks)
     if (hipFreeAsync(b.p, b.s) != hipSuccess) rc = sfail(FDCN_EHIP, "hipFreeAsync failed");
-  for (hipStream_t st : s->streams) {
+  for (hipStream_t st : s->streams)
     if (hipStreamSynchronize(st) != hipSuccess) rc = sfail(FDCN_EHIP, "stream sync failed");
-    (void)hipStreamDestroy(st);
-  }
-  for (hipEvent_t e : s->events) (void)hipEventDestroy(e);
-  s->pinned.release();
+  if (rc == FDCN_OK) {  // everything drained: the resources go back to the thread
+    for (hipEvent_t e : s->events) s->ctx->spare_events.push_back(e);
+    s->ctx->pinned.reset();
+    t_idle_ctx.push_back(s->ctx);
+  }  // after a failure they are dropped (leaked) rather than reused
   if (cur != s->device) (void)hipSetDevice(cur);
   delete s;
   return rc;
@@ -502,7 +542,7 @@ int fdcn_session_march(fdcn_session* s, int32_t it, int32_t B, int32_t n_nodes, 
   const size_t ws_bytes = (size_t)ws_ * (size_t)B;
   const size_t oW = L.add(ws_bytes);
 
-  char* h = s->pinned.get(staged);
+  char* h = s->pinned().get(staged);
   if (!h) return sfail(FDCN_ENOMEM, "hipHostMalloc(%zu) failed", staged);
   memcpy(h + oP, params, sizeof(double) * B * FDCN_NPARAM);
   memcpy(h + oI, iparams, sizeof(int32_t) * B * FDCN_NIPARAM);
@@ -564,7 +604,7 @@ int fdcn_session_dividend_jump(fdcn_session* s, int32_t B, int32_t n_nodes,
   const size_t staged = L.size;
   const size_t oO = L.add(sizeof(double) * nv);
   const size_t oW = L.add(sizeof(double) * 3 * nv);
-  char* h = s->pinned.get(staged);
+  char* h = s->pinned().get(staged);
   if (!h) return sfail(FDCN_ENOMEM, "hipHostMalloc(%zu) failed", staged);
   uint64_t* a = (uint64_t*)(h + oA);
   for (int32_t b = 0; b < B; ++b) a[b] = (uint64_t)s->slot_ptr[in_slots[b]];
@@ -623,7 +663,7 @@ int fdcn_session_greeks(fdcn_session* s, int32_t T, const int32_t* kind, const i
   const size_t oP = L.add(sizeof(double) * T * FDCN_GK_NPARAM);
   const size_t staged = L.size;
   const size_t oO = L.add(sizeof(double) * T * FDCN_GK_NOUT);
-  char* h = s->pinned.get(L.size);
+  char* h = s->pinned().get(L.size);
   if (!h) return sfail(FDCN_ENOMEM, "hipHostMalloc(%zu) failed", L.size);
   uint64_t* a = (uint64_t*)(h + oA);
   for (int32_t r = 0; r < R; ++r) a[r] = (uint64_t)s->slot_ptr[slots[r]];
@@ -663,7 +703,7 @@ int fdcn_session_fetch(fdcn_session* s, int32_t n, const int32_t* slots, int32_t
   Layout L;
   const size_t oA = L.add(sizeof(uint64_t) * n);
   const size_t oO = L.add(bytes);
-  char* h = s->pinned.get(L.size);
+  char* h = s->pinned().get(L.size);
   if (!h) return sfail(FDCN_ENOMEM, "hipHostMalloc(%zu) failed", L.size);
   uint64_t* a = (uint64_t*)(h + oA);
   for (int32_t i = 0; i < n; ++i) a[i] = (uint64_t)s->slot_ptr[slots[i]];

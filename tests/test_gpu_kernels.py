@@ -119,7 +119,11 @@ def test_batch_size_picks_variant():
     large = capi.plan(4097, False, B=4096)
     small = capi.plan(4097, False, B=1)
     assert (large["waves"], large["npt"]) == (1, 64)
+    # a single solve of 64-node chunks is split over 4 waves (latency)
     assert (small["waves"], small["npt"]) == (4, 16)
+    # a single 2049-node IT solve keeps W = 1 NPT = 32 (single-trade flavour)
+    one = capi.plan(2049, True, B=1)
+    assert (one["waves"], one["npt"]) == (1, 32)
 
 
 def test_large_batch_partial_block():

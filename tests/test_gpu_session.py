@@ -1,7 +1,7 @@
 """Device-resident sessions (csrc/fdcn_session.hip, session.py) on the MI355X.
 
 * a march in a session gives the host-array ABI's vectors bitwise (same
-  kernel); chained marches (v_init from slots) equal one long march;
+  kernel); chained marches (v_init from slots) equal the oracle's segments;
 * the device dividend jump is bit-identical to fdcn_dividend_jump (the host C
   restatement of fd_american_equity.py:479-553, :732-772, itself bitwise the
   NumPy/reference spline);
@@ -50,10 +50,11 @@ def test_session_march_and_fetch_equal_host_abi():
             assert np.array_equal(got, r)
 
 
-def test_chained_marches_equal_one_march():
-    """Two launches of n/2 steps, the second starting from the first's slots
-    (no Rannacher restart, tau0 carried), equal one n-step launch on the
-    IT path when tau is accumulated (tau mode 1 makes the split exact)."""
+def test_chained_marches_equal_two_oracle_segments():
+    """Two IT launches of n/2 steps, the second starting from the first's
+    slots (no Rannacher restart, tau0 carried on, accumulated tau), equal the
+    oracle marching the same two segments (the multiplier restarts at 0 at
+    each segment, as _solve_segment's does)."""
     rng = np.random.default_rng(8)
     n_time = 60
     full = [random_solve(rng, 513, n_time, 2, it=True) for _ in range(3)]
