@@ -28,6 +28,11 @@ metric line, ms per trade):
   trade_american  configs[1]: AmericanFDMPricer price_log2() + greeks_log2()
                   of the notebook trade, 2048 x 4096 (6 unique solves)
   trade_double    configs[4]: FDDoubleBarrier.price(b, r, T), 4096 x 8192
+Whole scenario file (run_all_scenarios' pricing, ms per file; host time split
+out -- VERDICT r1 item 7):
+  scenario_file   configs[2] numerics: 10 000 rows (KO / KI / vanilla, one
+                  option type per file), explicit 1024 x 2000, priced by
+                  scenario_batch.price_columns + result_columns
 
 value = total node-steps (configured nodes x steps x B x ranks) / max-over-
 ranks wall time of the K timed launches (whole-job aggregate).
@@ -70,7 +75,7 @@ N_SIMD = 1024
 BYTES_PER_NODE_STEP = {True: 32, False: 16}   # IT: V and lambda in+out; CN: V in+out
 FLOPS_PER_NODE_STEP = {True: 17, False: 10}
 DEFAULT_BATCH = {"american": 4096, "barrier": 10000, "double": 2048, "analytic": 1 << 20}
-TRADE_WORKLOADS = ("trade_cnlog", "trade_american", "trade_double")
+TRADE_WORKLOADS = ("trade_cnlog", "trade_american", "trade_double", "scenario_file")
 KERNEL_SRC = os.path.join(ROOT, "finite_difference_amd", "csrc", "fdcn_kernels.hip")
 
 
@@ -319,6 +324,8 @@ def spawn_ranks(args, argv) -> int:
 def run_rank(args):
     if args.workload == "analytic":
         return bench_analytic(args)
+    if args.workload == "scenario_file":
+        return bench_scenario_file(args)
     if args.workload in TRADE_WORKLOADS:
         return bench_trade(args)
     import numpy as np
@@ -507,6 +514,65 @@ def dry_run_rank(args, world: int, rank: int, local: int):
 # ---------------------------------------------------------------------------
 # single-trade latency through the drop-in facades
 # ---------------------------------------------------------------------------
+def bench_scenario_file(args):
+    """A 10 000-row scenario file priced end to end per step: native plan
+    build for every row, one launch of the 2R solves, the device Greeks
+    epilogue, the vectorised Black-76 legs and the result columns."""
+    import numpy as np
+    from finite_difference_amd import capi, distributed, scenario_batch, scenarios
+    from finite_difference_amd.engine import Engine
+    if distributed.bind_device() is None:
+        raise capi.FdcnError("no gfx950 device visible; the benchmark needs an MI355X")
+    R = args.batch or 10000
+    N, M = args.n_space or 1024, args.n_time or 2000
+    rng = np.random.default_rng(20250728)
+    kinds = ["up-and-out", "down-and-out", "up-and-in", "down-and-in", "none"]
+    S0 = 229.74
+    bt = [kinds[i % 5] for i in range(R)]
+    cols = {"scenario_name": [f"s{i}" for i in range(R)], "S0": [S0] * R,
+            "K": rng.uniform(150, 300, R).tolist(), "sigma": rng.uniform(0.15, 0.45, R).tolist(),
+            "rate": [(0.073086, 0.065)[i % 2] for i in range(R)], "barrier_type": bt,
+            "upper_barrier": [float(x) if "up" in b else None
+                              for b, x in zip(bt, rng.uniform(1.02, 1.5, R) * S0)],
+            "lower_barrier": [float(x) if "down" in b else None
+                              for b, x in zip(bt, rng.uniform(0.6, 0.98, R) * S0)],
+            "FA_price": [1.0] * R, "FA_delta": [0.5] * R, "FA_gamma": [0.01] * R,
+            "FA_vega": [0.2] * R}
+    base = scenarios.runner_base_params("put", N)
+    base.update(num_time_steps=M, grid_mode="explicit")
+    eng = Engine()
+
+    def one(timing):
+        res = scenario_batch.price_columns(cols, base, eng, timing=timing)
+        return scenario_batch.result_columns(cols, res)
+    for _ in range(args.warmup):
+        one({})
+    walls, plans, marches = [], [], []
+    out = None
+    for _ in range(args.steps):
+        tm = {}
+        t0 = time.perf_counter()
+        out = one(tm)
+        walls.append(time.perf_counter() - t0)
+        plans.append(tm["plan"])
+        marches.append(tm["march"])
+    ms = sum(walls) / len(walls) * 1e3
+    march_ms = sum(marches) / len(marches) * 1e3
+    n_pde = sum(1 for b in bt if b != "none")
+    print(json.dumps({
+        "metric": "scenario file wall time (run_all_scenarios pricing)",
+        "value": ms, "unit": "ms/file", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "ms_min": min(walls) * 1e3,
+        "higher_is_better": False, "scaling": "none", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic scenario file (config_scenarios.csv trade swept over K, sigma, "
+                "barriers; two curves)",
+        "config": {"workload": f"scenario_file_{R}rows_{N}x{M}", "config": "BASELINE configs[2]",
+                   "rows": R, "pde_rows": n_pde, "solves": 2 * n_pde},
+        "host_ms": ms - march_ms, "plan_ms": sum(plans) / len(plans) * 1e3,
+        "march_and_epilogue_ms": march_ms,
+        "outputs_finite": bool(np.all(np.isfinite(out["model_price"])))}), flush=True)
+
+
 def bench_trade(args):
     """One trade end to end per step: construct the facade, price (and for
     the American trade the Greeks), read the result -- host plan building,

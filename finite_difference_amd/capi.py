@@ -7,6 +7,7 @@ solve is requested, the call raises.
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import threading
 from typing import Optional
@@ -39,7 +40,8 @@ EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batc
             "fdcn_tau_sequence", "fdcn_tau_runs", "fdcn_session_create",
             "fdcn_session_destroy", "fdcn_session_slots", "fdcn_session_march",
             "fdcn_session_dividend_jump", "fdcn_session_greeks", "fdcn_session_fetch",
-            "fdcn_vc_batch", "fdcn_vc_batch_dev", "fdcn_vc_plan")
+            "fdcn_vc_batch", "fdcn_vc_batch_dev", "fdcn_vc_plan", "fdcn_barrier_plan",
+            "fdcn_vmath")
 VC_NDIAG = 6
 RR_NPARAM, RR_NFLAG = 8, 5
 DB_NPARAM, DB_NFLAG = 8, 3
@@ -133,6 +135,12 @@ def lib() -> ctypes.CDLL:
                                             _I64, _V]
             L.fdcn_vc_plan.restype = _I
             L.fdcn_vc_plan.argtypes = [_I, _I, _PI, _PI, ctypes.POINTER(ctypes.c_int64)]
+            L.fdcn_barrier_plan.restype = _I
+            L.fdcn_barrier_plan.argtypes = [_I, _V, _V, ctypes.c_double, _I, _I, _I, _I,
+                                            ctypes.c_double, ctypes.c_double, _I, _I, _V, _V,
+                                            _V, _V, _V, _V, _V, _V, _V]
+            L.fdcn_vmath.restype = _I
+            L.fdcn_vmath.argtypes = [_I, ctypes.c_int64, _V, _V]
             L.fdcn_select_device.restype = ctypes.c_int
             L.fdcn_select_device.argtypes = [_I]
             L.fdcn_current_device.restype = ctypes.c_int
@@ -276,6 +284,59 @@ def vc_plan(n_nodes: int, *, B: int) -> dict:
     ws = ctypes.c_int64()
     _check(lib().fdcn_vc_plan(B, n_nodes, ctypes.byref(w), ctypes.byref(npt), ctypes.byref(ws)))
     return dict(waves=w.value, npt=npt.value, ws_bytes_per_scen=ws.value)
+
+
+VM_EXP, VM_LOG, VM_SQRT, VM_SQUARE = 0, 1, 2, 3
+
+
+def vmath(op: int, x) -> np.ndarray:
+    """libm exp / log / sqrt / pow(x, 2) elementwise (bit-identical to CPython's
+    math.exp / math.log / math.sqrt and float ** 2), host only."""
+    X = _f64(x)
+    Y = np.empty_like(X)
+    _check(lib().fdcn_vmath(int(op), X.size, X.ctypes.data, Y.ctypes.data))
+    return Y
+
+
+BP_NROW, BP_NFLAG = 10, 4  # FDCN_BP_NROW / FDCN_BP_NFLAG
+GK_NPARAM, GK_NRINT, GK_NRDBL = 8, 5, 8
+
+
+def barrier_plan(row: np.ndarray, flag: np.ndarray, T: float, n_space: int, n_time: int,
+                 grid_mode: int, k_tail: float, dv_sigma: float,
+                 rebate_at_hit: bool, mon_k: np.ndarray) -> dict:
+    """fdcn_barrier_plan: base and sigma-bumped solve of every row (solve
+    q = 2 row + bump), host only.  Returns the launch arrays (params, iparams,
+    v_init, mon_rebate), the readouts (rint with the solve index in column 0,
+    rdbl), the per-row epilogue parameters and n_nodes."""
+    row = np.ascontiguousarray(row, np.float64)
+    flag = np.ascontiguousarray(flag, np.int32)
+    R = row.shape[0]
+    if row.shape != (R, BP_NROW) or flag.shape != (R, BP_NFLAG):
+        raise ValueError("barrier_plan: row [R, 10] and flag [R, 4] expected")
+    mon = np.ascontiguousarray(mon_k, np.int32)
+    if grid_mode == 0:
+        n_max = int(math.ceil(k_tail * n_time)) + 2
+    else:
+        n_max = int(n_space)
+    Q = 2 * R
+    out = dict(params=np.empty((Q, NPARAM)), iparams=np.empty((Q, NIPARAM), np.int32),
+               v_init=np.empty(Q * n_max), mon_rebate=np.empty(max(1, Q * mon.size)),
+               rint=np.empty((Q, GK_NRINT), np.int32), rdbl=np.empty((Q, GK_NRDBL)),
+               tparams=np.empty((R, GK_NPARAM)))
+    nn = np.zeros(1, np.int32)
+    _check(lib().fdcn_barrier_plan(
+        R, row.ctypes.data, flag.ctypes.data, float(T), int(n_space), int(n_time),
+        int(grid_mode), n_max, float(k_tail), float(dv_sigma), 1 if rebate_at_hit else 0,
+        mon.size, mon.ctypes.data if mon.size else None, out["params"].ctypes.data,
+        out["iparams"].ctypes.data, out["v_init"].ctypes.data, out["mon_rebate"].ctypes.data,
+        out["rint"].ctypes.data, out["rdbl"].ctypes.data, out["tparams"].ctypes.data,
+        nn.ctypes.data))
+    N = int(nn[0])
+    out["n_nodes"] = N
+    out["v_init"] = out["v_init"][:Q * N].reshape(Q, N)
+    out["mon_rebate"] = out["mon_rebate"][:Q * mon.size]
+    return out
 
 
 def log_grid(x_min: float, dx: float, n: int):

@@ -224,16 +224,30 @@ def run_all_scenarios(config_csv_path: str, output_csv_path: Optional[str],
     torch.distributed is initialised."""
     import pandas as pd
     from . import distributed
+    from . import scenario_batch
     cfg = pd.read_csv(config_csv_path)
-    rows = [dict(r) for _, r in cfg.iterrows()]
     if distributed.is_initialized():
         distributed.bind_device()  # this rank's GPU (LOCAL_RANK), before any launch
+    if distributed.rank_world()[1] == 1:
+        # the whole file in one plan build + one launch (scenario_batch.py)
+        cols = {k: cfg[k].tolist() for k in scenario_batch.ROW_KEYS if k in cfg.columns}
+        priced = scenario_batch.price_columns(cols, base_params, engine)
+        if priced is not None:
+            df = pd.DataFrame(scenario_batch.result_columns(cols, priced))
+            res = df.to_dict("records") if verbose else None
+            return _finish_scenarios(df, res, output_csv_path, verbose)
+    rows = [dict(r) for _, r in cfg.iterrows()]
     mine = distributed.shard(rows)
-    res = run_rows_batched(mine, base_params, engine)
+    res = scenario_batch.run_rows_vectorized(mine, base_params, engine)
+    if res is None:
+        res = run_rows_batched(mine, base_params, engine)
     res = distributed.gather_rows(res)
     if res is None:  # non-zero rank
         return None
-    df = pd.DataFrame(res)
+    return _finish_scenarios(pd.DataFrame(res), res, output_csv_path, verbose)
+
+
+def _finish_scenarios(df, res, output_csv_path, verbose):
     if verbose:
         for r in res:
             print(f"{r['scenario_name']}: Price %Diff: {r['price_pct_diff']:.4f}%, "

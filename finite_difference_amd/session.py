@@ -183,8 +183,22 @@ class Session:
             for r in rds:
                 rint.append((r.slot, r.icase, r.ilo, r.idx, r.dg_mode))
                 rdbl.append(r.dbl)
-        RI = np.ascontiguousarray(np.array(rint, np.int32).reshape(-1, GK_NRINT))
-        RD = np.ascontiguousarray(np.array(rdbl, np.float64).reshape(-1, GK_NRDBL))
+        return self.greeks_raw(kind, first, tp, np.array(rint, np.int32).reshape(-1, GK_NRINT),
+                               np.array(rdbl, np.float64).reshape(-1, GK_NRDBL))
+
+    def greeks_raw(self, kind, first, tparams, rint, rdbl) -> np.ndarray:
+        """The epilogue on flat arrays (include/fdcn.h layout): kind [T],
+        first readout [T], tparams [T, GK_NPARAM], rint [n, GK_NRINT] (slot
+        first), rdbl [n, GK_NRDBL] -> [T, 6]."""
+        kind = np.ascontiguousarray(kind, np.int32)
+        first = np.ascontiguousarray(first, np.int32)
+        T = kind.shape[0]
+        tp = np.ascontiguousarray(tparams, np.float64)
+        RI = np.ascontiguousarray(rint, np.int32)
+        RD = np.ascontiguousarray(rdbl, np.float64)
+        if (first.shape != (T,) or tp.shape != (T, GK_NPARAM) or RI.ndim != 2
+                or RI.shape[1] != GK_NRINT or RD.shape != (RI.shape[0], GK_NRDBL)):
+            raise ValueError("greeks_raw: array shapes do not match the fdcn.h layout")
         out = np.empty((T, GK_NOUT))
         capi._check(self._L.fdcn_session_greeks(self._h, T, _ptr(kind), _ptr(first), _ptr(tp),
                                                 RI.shape[0], _ptr(RI), _ptr(RD), _ptr(out)))

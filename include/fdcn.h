@@ -333,6 +333,43 @@ int fdcn_tau_runs(double tau0, double dt, int32_t n);
 int fdcn_dividend_jump(int32_t n, const double* s, const double* v, double cash_div,
                        double strike_call, double* v_out);
 
+/* ---- whole-file plan builder (finite_difference_amd/csrc/fdcn_plan.hip) --
+ * The discrete-barrier scenario runner's per-row work (run_config_scenarios.py
+ * :137-195 over DiscreteBarrierFDMPricer: choose_grid_parameters, the log
+ * grid, payoff, boundaries, knock-out thresholds, monitoring rebates and the
+ * operator coefficients of the base and sigma-bumped solves, …pricer.py
+ * :270-547, :883-904) for R rows at once, with libm's exp/log/sqrt and the
+ * reference's operation order: the plan arrays are bit-identical to the
+ * per-row facade's.  Output solve q = 2*row + (0 base, 1 bumped by dv_sigma):
+ *   params [2R][FDCN_NPARAM], iparams [2R][FDCN_NIPARAM] (monitor run q*n_mon),
+ *   v_init [2R][N] (N = the grid's N_s, the march's n_nodes: *n_nodes_out),
+ *   mon_rebate [2R][n_mon] (steps: mon_k, shared by all rows),
+ *   rint / rdbl [2R] readouts in fdcn_session_greeks layout (slot field = q),
+ *   tparams [R][FDCN_GK_NPARAM] (FDCN_GK_BARRIER, readouts 2*row, 2*row+1).
+ * v_init holds 2R * n_nodes_cap doubles; FDCN_EINVAL (nothing written) if
+ * N > n_nodes_cap or the rows' N differ (parity mode N = ceil(k_tail n_time)
+ * up to rounding, explicit mode N = n_space).  grid_mode 0 parity, 1 explicit. */
+#define FDCN_BP_NROW 10
+enum fdcn_bp_row {
+  FDCN_BP_SPOT = 0, FDCN_BP_STRIKE, FDCN_BP_SIGMA, FDCN_BP_LO, FDCN_BP_UP,
+  FDCN_BP_CARRY, FDCN_BP_DIVY, FDCN_BP_DISC, FDCN_BP_PV, FDCN_BP_REBATE
+};
+#define FDCN_BP_NFLAG 4
+enum fdcn_bp_flag {
+  FDCN_BP_PUT = 0, /* 1 for puts */
+  FDCN_BP_KO,      /* 1 down-and-out, 2 up-and-out, 3 double-out (knock-ins: their twin) */
+  FDCN_BP_HAS_LO, FDCN_BP_HAS_UP
+};
+int fdcn_barrier_plan(int32_t R, const double* row, const int32_t* rflag, double T,
+                      int32_t n_space, int32_t n_time, int32_t grid_mode, int32_t n_nodes_cap,
+                      double k_tail, double dv_sigma, int32_t rebate_at_hit, int32_t n_mon,
+                      const int32_t* mon_k, double* params, int32_t* iparams, double* v_init,
+                      double* mon_rebate, int32_t* rint, double* rdbl, double* tparams,
+                      int32_t* n_nodes_out);
+/* y = exp(x) (op 0), log(x) (1), sqrt(x) (2), pow(x, 2.0) (3) elementwise with
+ * the C library (the functions CPython's math module and float ** call). */
+int fdcn_vmath(int32_t op, int64_t n, const double* x, double* y);
+
 const char* fdcn_last_error(void);
 int fdcn_device_count(void);   /* gfx950 devices visible; 0 if none          */
 int fdcn_abi_version(void);    /* FDCN_ABI_VERSION                           */

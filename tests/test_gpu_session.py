@@ -197,3 +197,46 @@ def test_prefetch_many_device_matches_single_trades():
         one = T.make(c, Engine())
         assert p.price_log2() == one.price_log2()
         assert p.greeks_log2() == one.greeks_log2()
+
+
+@pytest.mark.parametrize("opt", ["put", "call"])
+def test_vectorized_scenario_file_equals_batched_runner(opt):
+    """scenario_batch (native plan, one launch, device epilogue) against
+    run_rows_batched on the same GPU: the same 2R solves in the same order,
+    so bitwise; and the host epilogue over the same vectors, bitwise."""
+    import math
+    import test_scenario_batch as T
+    from finite_difference_amd import scenario_batch
+    base = scenarios.runner_base_params(opt, 64)
+    base.update(num_time_steps=40, grid_mode="explicit", rebate_amount=0.5)
+    rows = T._rows(40, 9)
+    a = scenarios.run_rows_batched(rows, base, Engine())
+    b = scenario_batch.run_rows_vectorized(rows, base, Engine())
+    c = scenario_batch.run_rows_vectorized(rows, base, host_engine())
+    for ra, rb, rc in zip(a, b, c):
+        for k in ra:
+            for x in (rb, rc):
+                same = ra[k] == x[k] or (isinstance(ra[k], float) and math.isnan(ra[k])
+                                         and math.isnan(x[k]))
+                assert same, (ra["scenario_name"], k, ra[k], x[k])
+
+
+def test_run_all_scenarios_file_on_device(tmp_path):
+    """run_all_scenarios takes the vectorised path for a whole CSV and writes
+    the per-row runner's numbers (oracle engine) to within the kernel's
+    tolerance."""
+    import pandas as pd
+    import test_scenario_batch as T
+    from backends import oracle_engine
+    rows = T._rows(25, 4)
+    cfg = tmp_path / "cfg.csv"
+    pd.DataFrame(rows).to_csv(cfg, index=False)
+    base = scenarios.runner_base_params("put", 64)
+    base.update(num_time_steps=40, grid_mode="explicit")
+    df = scenarios.run_all_scenarios(str(cfg), str(tmp_path / "out.csv"), base, Engine(),
+                                     verbose=False)
+    ref = scenarios.run_rows(rows, base, oracle_engine())
+    assert len(df) == len(ref)
+    for i, r in enumerate(ref):
+        for k in ("model_price", "model_delta", "model_gamma", "model_vega"):
+            assert abs(df[k].iloc[i] - r[k]) <= 1e-9 * max(1.0, abs(r[k])), (i, k)
