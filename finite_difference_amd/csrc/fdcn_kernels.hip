@@ -302,6 +302,13 @@ struct KoLoad {
   static constexpr bool value = !IT && NPT >= 48;
 };
 
+// CN variants marched in the split form (state V, solve into T; see the step
+// forms in fdcn_march).  Their workspace row also holds the raw Dirichlet
+// values of every step (read back only after a knock-out step).
+__host__ __device__ constexpr bool split_form(int it, int w, int npt) {
+  return !it && (w == 16 ? npt <= 16 : npt <= 40);
+}
+
 // CN variants marched in the recovery form (W = 1, NPT > 40; see the step
 // forms in fdcn_march).  Their Rannacher steps keep the old V in a
 // workspace slice [64][NPT] per scenario (host: ws_bytes_per_scen).
@@ -321,7 +328,7 @@ struct KArgs {
   const int32_t* mon_step;
   const double* mon_rebate;
   double* v_out;
-  double* bnd;      // workspace: Dirichlet values [B][W][n_pad + kKoRow][2]
+  double* bnd;      // workspace: Dirichlet terms [B][W][n_pad + kKoRow (+ n_pad split form)][2]
   double* zg;       // workspace: correction tables [B][2][lz][NPT+1] (ZG variants)
   double* vsave;    // workspace: old V of a Rannacher step [B][64][NPT] (rec_form variants)
   int n_pad;        // n_time rounded up to a multiple of 64
@@ -406,8 +413,9 @@ fdcn_march(KArgs A) {
   // theta-form rhs term (-A_L)(lo_m + c2 lo_{m-1}) / (-A_U)(hi_m + c2 hi_{m-1})
   // (see the IT rhs below); IT has no knock-out, so lo_{m-1} is simply the
   // previous step's value and the whole term is tabulated here.
-  double2* bnd =
-      reinterpret_cast<double2*>(A.bnd) + ((size_t)scen * W + wave) * (A.n_pad + kKoRow);
+  double2* bnd = reinterpret_cast<double2*>(A.bnd) +
+                 ((size_t)scen * W + wave) *
+                     (A.n_pad + kKoRow + (split_form(IT, W, NPT) ? A.n_pad : 0));
   const int lof = uni_i(I[FDCN_I_LO_FORM]), hif = uni_i(I[FDCN_I_HI_FORM]);
   const double l0 = uni(P[FDCN_P_LO_C0]), l1 = uni(P[FDCN_P_LO_E0]), l2 = uni(P[FDCN_P_LO_C1]),
                l3 = uni(P[FDCN_P_LO_E1]);
@@ -434,9 +442,19 @@ fdcn_march(KArgs A) {
     }
     __threadfence_block();
   }
+  // Split-form CN (kSplit below) tabulates its rhs terms too: th (-A_L)(lo_new
+  // + c2 lo_prev) with lo_prev the previous step's Dirichlet value, the
+  // expression and operand order of the in-loop form it replaces (bitwise the
+  // same numbers).  A knock-out that removes node 0 or the last node sets
+  // lo_prev / hi_prev to the rebate instead: the step after one recomputes
+  // its term from the raw values, kept in a second table (bnd_raw).
+  constexpr bool kTabSplit = split_form(IT, W, NPT);
+  double2* bnd_raw = bnd + A.n_pad + kKoRow;  // kTabSplit only
+  (void)bnd_raw;
   {
     const double* vb = A.v_init + (size_t)scen * n_nodes;
-    const double v_lo0 = IT ? uni(vb[0]) : 0.0, v_hi0 = IT ? uni(vb[n_nodes - 1]) : 0.0;
+    const double v_lo0 = (IT || kTabSplit) ? uni(vb[0]) : 0.0;
+    const double v_hi0 = (IT || kTabSplit) ? uni(vb[n_nodes - 1]) : 0.0;
     for (int m = lane; m < A.n_pad; m += 64) {
       double tau = tau0 + (double)(m + 1) * dt, tp = tau0 + (double)m * dt;
       if (tau_mode == 1) {
@@ -452,6 +470,15 @@ fdcn_march(KArgs A) {
         const double th = m < A.n_ranna ? 1.0 : 0.5;
         const double c2 = (1.0 - th) / th;  // Phase::c2, pl, pu for this step's theta
         bnd[m] = make_double2((th * dt * ca) * fma(c2, lo_p, lo), (th * dt * cc) * fma(c2, hi_p, hi));
+      } else if constexpr (kTabSplit) {
+        // Phase::th, pl, pu, c2 of this step's theta (make_phase)
+        const double lo_p = m == 0 ? v_lo0 : bnd_eval(lof, l0, l1, l2, l3, tp);
+        const double hi_p = m == 0 ? v_hi0 : bnd_eval(hif, h0, h1, h2, h3, tp);
+        const double th = m < A.n_ranna ? 1.0 : 0.5;
+        const double AL = -th * dt * ca, AU = -th * dt * cc;
+        const double c2 = (1.0 - th) / th;
+        bnd[m] = make_double2(th * (-AL * fma(c2, lo_p, lo)), th * (-AU * fma(c2, hi_p, hi)));
+        bnd_raw[m] = make_double2(lo, hi);
       } else {
         bnd[m] = make_double2(lo, hi);
       }
@@ -511,7 +538,7 @@ fdcn_march(KArgs A) {
   //   CN, stencil   state V, 3-point rhs in place (shifted layout); the
   //                 multi-wave variants whose V + T would not fit the
   //                 register budget
-  constexpr bool kSplit = !IT && (W == 16 ? NPT <= 16 : NPT <= 40);
+  constexpr bool kSplit = kTabSplit;
   // CN, recover (W = 1, NPT > 40): state V only, pointwise rhs V solved in
   // place; the update x = s u - c2 V needs the old V, which the last
   // backward pass recovers from the forward-pass values it is about to
@@ -621,9 +648,9 @@ fdcn_march(KArgs A) {
     double a[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      double w = 0.0;
+      double w = In(j * M);  // zero carry: the first FMA is the input itself
 #pragma unroll
-      for (int i = 0; i < M; ++i) {
+      for (int i = 1; i < M; ++i) {
         const int k = j * M + i;
         w = fma(k == NPT - 1 ? mlast : fm, w, In(k));
       }
@@ -673,9 +700,9 @@ fdcn_march(KArgs A) {
     // backward pass 1: zero-carry start value of every sub-chain
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      double y = 0.0;
+      double y = Wr(j * M + M - 1);  // zero carry
 #pragma unroll
-      for (int i = M - 1; i >= 0; --i) {
+      for (int i = M - 2; i >= 0; --i) {
         const int k = j * M + i;
         y = fma(k == NPT - 1 ? glast : bm, y, Wr(k));
       }
@@ -912,6 +939,8 @@ fdcn_march(KArgs A) {
       if (rh >= 0 && rh < 64) { kmh.part = 1ull << rh; kmh.k0 = sh; kmh.k1 = NPT - 1; }
     }
   }
+  const unsigned long long shrt_ballot = kSplit ? (unsigned long long)__ballot(shrt) : 0ull;
+  (void)shrt_ballot;
   unsigned long long kom_addr = 0;  // this wave's mask row (KoLoad variants)
   if constexpr (KoLoad<IT, NPT>::value) {
     unsigned long long* kom = reinterpret_cast<unsigned long long*>(bnd + A.n_pad);
@@ -984,6 +1013,8 @@ fdcn_march(KArgs A) {
 
   double2 bnd_cur = make_double2(0.0, 0.0);
   double2 bnd_nxt = bnd[lane];  // steps 0..63
+  int ko_prev = 0;  // kSplit: bit 0 / 1 -- the last step knocked out node 0 / the last node
+  (void)ko_prev;
   double halo_l = 0.0, halo_r = 0.0;
   if constexpr (W == 1 && !kNatural) {
     halo_l = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
@@ -1002,8 +1033,8 @@ fdcn_march(KArgs A) {
       bnd_cur = bnd_nxt;
       if (m + 64 < A.n_pad) bnd_nxt = bnd[m + 64 + lane];  // prefetch the block after
     }
-    const double lo_new = read_lane(bnd_cur.x, m & 63);
-    const double hi_new = read_lane(bnd_cur.y, m & 63);
+    double lo_new = read_lane(bnd_cur.x, m & 63);  // kSplit: the tabulated rhs terms
+    double hi_new = read_lane(bnd_cur.y, m & 63);
 
     // ---- 1. rhs ------------------------------------------------------------
     if constexpr (IT) {
@@ -1027,10 +1058,17 @@ fdcn_march(KArgs A) {
       // lo_old) e_0 + theta (-A_U)(hi_new + c2 hi_old) e_n.  The rhs is V
       // itself except at the two end nodes (vb0 / vb1); the solve reads V and
       // writes T, and x = (r u)/(theta r) - c2 V afterwards.
-      const double blo = ph.th * (ph.pl * fma(ph.c2, V0, lo_new));
-      const double bhi = ph.th * (ph.pu * fma(ph.c2, VN, hi_new));
+      double blo = lo_new, bhi = hi_new;
+      if (ko_prev) {  // after a knock-out step: terms from the rebate (uniform branch)
+        const double2 raw = bnd_raw[m];
+        if (ko_prev & 1) blo = ph.th * (ph.pl * fma(ph.c2, V0, uni(raw.x)));
+        if (ko_prev & 2) bhi = ph.th * (ph.pu * fma(ph.c2, VN, uni(raw.y)));
+        ko_prev = 0;
+      }
       vb0 = fma(e_first, blo, V[0]);
-      vb1 = shrt ? 0.0 : fma(e_last, bhi, V[NPT - 1]);  // knock-out may have set a phantom
+      // the phantom slot of a short lane is an exact zero and e_last is 0
+      // there (the update and the knock-out masks keep it so)
+      vb1 = fma(e_last, bhi, V[NPT - 1]);
     } else if constexpr (kRec) {
       // the kSplit rhs, in place (the phantom slot is kept at zero by the
       // update and by the knock-out masks)
@@ -1208,18 +1246,34 @@ fdcn_march(KArgs A) {
           }
         }
         if constexpr (kSplit) {
-          asm volatile(
-              "v_fma_f64 %4, %8, %9, %4\n\t"
-              "v_fma_f64 %5, %8, %10, %5\n\t"
-              "v_fma_f64 %6, %8, %11, %6\n\t"
-              "v_fma_f64 %7, %8, %12, %7\n\t"
-              "v_fma_f64 %0, %13, %4, -%0\n\t"
-              "v_fma_f64 %1, %13, %5, -%1\n\t"
-              "v_fma_f64 %2, %13, %6, -%2\n\t"
-              "v_fma_f64 %3, %13, %7, -%3"
-              : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(T[k]),
-                "+v"(T[k + 1]), "+v"(T[k + 2]), "+v"(T[k + 3])
-              : "v"(g), "v"(zk[0]), "v"(zk[1]), "v"(zk[2]), "v"(zk[3]), "s"(ph.s));
+          if (k + 4 < NPT) {
+            asm volatile(
+                "v_fma_f64 %4, %8, %9, %4\n\t"
+                "v_fma_f64 %5, %8, %10, %5\n\t"
+                "v_fma_f64 %6, %8, %11, %6\n\t"
+                "v_fma_f64 %7, %8, %12, %7\n\t"
+                "v_fma_f64 %0, %13, %4, -%0\n\t"
+                "v_fma_f64 %1, %13, %5, -%1\n\t"
+                "v_fma_f64 %2, %13, %6, -%2\n\t"
+                "v_fma_f64 %3, %13, %7, -%3"
+                : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(T[k]),
+                  "+v"(T[k + 1]), "+v"(T[k + 2]), "+v"(T[k + 3])
+                : "v"(g), "v"(zk[0]), "v"(zk[1]), "v"(zk[2]), "v"(zk[3]), "s"(ph.s));
+          } else {
+            // the last slot takes s_l (0 on short lanes): the phantom stays zero
+            asm volatile(
+                "v_fma_f64 %4, %8, %9, %4\n\t"
+                "v_fma_f64 %5, %8, %10, %5\n\t"
+                "v_fma_f64 %6, %8, %11, %6\n\t"
+                "v_fma_f64 %7, %8, %12, %7\n\t"
+                "v_fma_f64 %0, %13, %4, -%0\n\t"
+                "v_fma_f64 %1, %13, %5, -%1\n\t"
+                "v_fma_f64 %2, %13, %6, -%2\n\t"
+                "v_fma_f64 %3, %14, %7, -%3"
+                : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(T[k]),
+                  "+v"(T[k + 1]), "+v"(T[k + 2]), "+v"(T[k + 3])
+                : "v"(g), "v"(zk[0]), "v"(zk[1]), "v"(zk[2]), "v"(zk[3]), "s"(ph.s), "v"(s_l));
+          }
         } else if constexpr (kRec) {
           // V holds s u already (both phases): x = s u + (s g) z
 #pragma unroll
@@ -1262,10 +1316,7 @@ fdcn_march(KArgs A) {
         }
       }
     }
-    if constexpr (kSplit) {
-      if (shrt) V[NPT - 1] = 0.0;
-    }
-    if constexpr (!IT) {  // IT reads the tabulated terms instead
+    if constexpr (!IT && !kSplit) {  // IT and kSplit read tabulated terms instead
       V0 = lo_new;
       VN = hi_new;
     }
@@ -1334,8 +1385,9 @@ fdcn_march(KArgs A) {
       } else {
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
-        const unsigned long long mk = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) |
-                                      kmh.full | ((k >= kmh.k0 && k <= kmh.k1) ? kmh.part : 0ull);
+        unsigned long long mk = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) |
+                                kmh.full | ((k >= kmh.k0 && k <= kmh.k1) ? kmh.part : 0ull);
+        if (kSplit && k == NPT - 1) mk &= ~shrt_ballot;  // the phantom stays zero
         unsigned lo = (unsigned)__double_as_longlong(V[k]);
         unsigned hi = (unsigned)(__double_as_longlong(V[k]) >> 32);
         const unsigned rlo = (unsigned)__double_as_longlong(rebv);
@@ -1349,6 +1401,7 @@ fdcn_march(KArgs A) {
       }
       if (0 <= ko_lo) V0 = reb;
       if (n_nodes - 1 >= ko_hi) VN = reb;
+      if constexpr (kSplit) ko_prev = (0 <= ko_lo ? 1 : 0) | (n_nodes - 1 >= ko_hi ? 2 : 0);
       // advance to the prefetched entry; request the one after it
       ++mpos;
       next_mon = mpos < mend ? pf_mon : 0x7fffffff;
@@ -1380,6 +1433,12 @@ fdcn_march(KArgs A) {
     if (A.n_time > 0) {
       V0 = bnd_eval(lof, l0, l1, l2, l3, tau_end);
       VN = bnd_eval(hif, h0, h1, h2, h3, tau_end);
+    }
+  }
+  if constexpr (kSplit) {  // likewise, unless the last step knocked the node out
+    if (A.n_time > 0) {
+      if (!(ko_prev & 1)) V0 = bnd_eval(lof, l0, l1, l2, l3, tau_end);
+      if (!(ko_prev & 2)) VN = bnd_eval(hif, h0, h1, h2, h3, tau_end);
     }
   }
   // ---- store ---------------------------------------------------------------
@@ -1552,11 +1611,13 @@ int lds_doubles(const Variant& v, int lz) { return v.lds_per_scen(lz) * v.spb; }
 int pad64(int n) { return ((n > 0 ? n : 1) + 63) / 64 * 64; }
 
 // workspace bytes per scenario: one (lo, hi) Dirichlet pair per step and
-// wave plus the knock-out mask row (kKoRow) of each wave;
+// wave plus the knock-out mask row (kKoRow) of each wave (split-form
+// variants: a second pair per step, the raw values behind their rhs terms);
 // ZG variants add the correction table [2][lz][NPT+1], rec_form variants
 // the Rannacher save slice [64][NPT]
 size_t bnd_bytes_per_scen(const Variant& v, int n_time) {
-  return sizeof(double) * 2 * (size_t)(pad64(n_time) + kKoRow) * (size_t)v.w;
+  const size_t row = (size_t)pad64(n_time) * (split_form(v.it, v.w, v.npt) ? 2 : 1) + kKoRow;
+  return sizeof(double) * 2 * row * (size_t)v.w;
 }
 size_t zg_bytes_per_scen(const Variant& v, int lz) {
   return v.zg ? sizeof(double) * 2 * (size_t)lz * (size_t)(v.npt + 1) : 0;

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Build libfdcn.so from the csrc/ + include/ of a git revision (or the working
+# tree for "WT") into ab/TAG/libfdcn.so, for A/B timing through FDCN_LIB
+# (bench.py / capi.py).  Usage: bash tools/build_ab.sh TAG [REV]
+set -euo pipefail
+TAG=$1; REV=${2:-WT}
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+SRC=$(mktemp -d)
+mkdir -p "$SRC/finite_difference_amd/csrc" "$SRC/include" "$ROOT/ab/$TAG"
+if [ "$REV" = "WT" ]; then
+  cp "$ROOT"/finite_difference_amd/csrc/*.hip "$SRC/finite_difference_amd/csrc/"
+  cp "$ROOT"/include/*.h "$SRC/include/"
+else
+  for f in $(git -C "$ROOT" ls-tree --name-only "$REV" finite_difference_amd/csrc/ include/); do
+    git -C "$ROOT" show "$REV:$f" > "$SRC/$f"
+  done
+fi
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared \
+    -o "$ROOT/ab/$TAG/libfdcn.so" "$SRC"/finite_difference_amd/csrc/*.hip
+rm -rf "$SRC"
+echo "$ROOT/ab/$TAG/libfdcn.so"
