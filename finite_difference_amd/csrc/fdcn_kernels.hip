@@ -73,6 +73,11 @@ __device__ __forceinline__ double read_lane(double x, int l) {
 }
 
 __device__ __forceinline__ int uni_i(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// the larger of lane 0's and lane 32's value (the two scenarios of a paired wave)
+__device__ __forceinline__ int umax_halves(int x) {
+  const int a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 32);
+  return a > b ? a : b;
+}
 
 // Hide an index from the optimiser for one loop iteration, so table loads
 // indexed by it are not hoisted out of the time loop (LICM would otherwise keep
@@ -147,8 +152,10 @@ struct Phase {
   double th;          // theta
 };
 
+template <bool kLane = false>  // kLane: per-lane (paired waves) instead of SGPR values
 __device__ __forceinline__ Phase make_phase(double theta, double dt, double a, double c,
                                             double bcoef) {
+  auto uni = [](double x) { return kLane ? x : ::uni(x); };
   // build_matrices(theta), discrete_barrier_fdm_pricer.py:475-484
   const double AL = -theta * dt * a;
   const double AC = 1.0 - theta * dt * bcoef;
@@ -286,6 +293,48 @@ struct KoMask {
   int k0, k1;
 };
 
+// One scenario's monitoring entries (wave-uniform): the entry of the next
+// knock-out step and the one after it, loaded a monitor step ahead of their
+// use so the scalar-load latency is off the step.
+struct MonRun {
+  int pos, end, next, pf;
+  double cur, pf_reb;
+  __device__ __forceinline__ void init(const int32_t* st, const double* rb, int start, int count) {
+    pos = start;
+    end = start + count;
+    // entries < 1 never match a step: skip them (the oracle's `while` does)
+    while (pos < end && uni_i(st[pos]) < 1) ++pos;
+    next = pf = 0x7fffffff;
+    cur = pf_reb = 0.0;
+    if (pos < end) {
+      next = uni_i(st[pos]);
+      cur = uni(rb[pos]);
+      if (pos + 1 < end) {
+        pf = uni_i(st[pos + 1]);
+        pf_reb = uni(rb[pos + 1]);
+      }
+    }
+  }
+  // after the knock-out at `step`: advance to the prefetched entry, request
+  // the one after it
+  __device__ __forceinline__ void advance(const int32_t* st, const double* rb, int step) {
+    ++pos;
+    next = pos < end ? pf : 0x7fffffff;
+    cur = pf_reb;
+    if (pos + 1 < end) {
+      pf = uni_i(st[pos + 1]);
+      pf_reb = uni(rb[pos + 1]);
+    }
+    if (next <= step) {  // entries not strictly increasing: skip (slow path)
+      while (pos < end && uni_i(st[pos]) <= step) ++pos;
+      next = (pos < end) ? uni_i(st[pos]) : 0x7fffffff;
+      cur = (pos < end) ? uni(rb[pos]) : 0.0;
+      pf = (pos + 1 < end) ? uni_i(st[pos + 1]) : 0x7fffffff;
+      pf_reb = (pos + 1 < end) ? uni(rb[pos + 1]) : 0.0;
+    }
+  }
+};
+
 // Each wave's workspace row ends in kKoRow double2 = 64 per-slot knock-out
 // masks.  For NPT >= 48 the NPT masks (2 NPT SGPRs) do not fit the scalar
 // file: the compiler spilled them to VGPR lanes and read each back with two
@@ -297,9 +346,9 @@ typedef unsigned KoMask16 __attribute__((ext_vector_type(16)));  // 8 masks, s_l
 __device__ __forceinline__ unsigned long long ko_pair(KoMask16 m, int j) {
   return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];
 }
-template <int IT, int NPT>
-struct KoLoad {
-  static constexpr bool value = !IT && NPT >= 48;
+template <int IT, int NPT, int ZG = 0>
+struct KoLoad {  // also the paired flavour: two scenarios' masks would crowd the scalar file
+  static constexpr bool value = !IT && (NPT >= 48 || (ZG & 4));
 };
 
 // CN variants marched in the split form (state V, solve into T; see the step
@@ -315,6 +364,40 @@ __host__ __device__ constexpr bool split_form(int it, int w, int npt) {
 __host__ __device__ constexpr bool rec_form(int it, int w, int npt) {
   return !it && w == 1 && npt > 40;
 }
+
+
+// The split-form update of four slots: T_i += g z_i, V_i = s T_i - V_i (last
+// slot scaled by s_last when kLast).  s in an SGPR pair, or a VGPR (kVs:
+// paired waves, whose scenarios have their own s).
+#define FDCN_SPLIT_UPD_ASM(S3)                                                     \
+  "v_fma_f64 %4, %8, %9, %4\n\t"                                                 \
+  "v_fma_f64 %5, %8, %10, %5\n\t"                                                \
+  "v_fma_f64 %6, %8, %11, %6\n\t"                                                \
+  "v_fma_f64 %7, %8, %12, %7\n\t"                                                \
+  "v_fma_f64 %0, %13, %4, -%0\n\t"                                               \
+  "v_fma_f64 %1, %13, %5, -%1\n\t"                                               \
+  "v_fma_f64 %2, %13, %6, -%2\n\t"                                               \
+  "v_fma_f64 %3, " S3 ", %7, -%3"
+#define FDCN_SPLIT_UPD_OUT "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(t0), "+v"(t1), "+v"(t2), "+v"(t3)
+template <bool kVs, bool kLast>
+__device__ __forceinline__ void split_update(double& v0, double& v1, double& v2, double& v3,
+                                             double& t0, double& t1, double& t2, double& t3,
+                                             double g, const double* z, double s, double s_last) {
+  if constexpr (!kVs && !kLast)
+    asm volatile(FDCN_SPLIT_UPD_ASM("%13") : FDCN_SPLIT_UPD_OUT
+                 : "v"(g), "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(z[3]), "s"(s));
+  else if constexpr (!kVs)
+    asm volatile(FDCN_SPLIT_UPD_ASM("%14") : FDCN_SPLIT_UPD_OUT
+                 : "v"(g), "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(z[3]), "s"(s), "v"(s_last));
+  else if constexpr (!kLast)
+    asm volatile(FDCN_SPLIT_UPD_ASM("%13") : FDCN_SPLIT_UPD_OUT
+                 : "v"(g), "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(z[3]), "v"(s));
+  else
+    asm volatile(FDCN_SPLIT_UPD_ASM("%14") : FDCN_SPLIT_UPD_OUT
+                 : "v"(g), "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(z[3]), "v"(s), "v"(s_last));
+}
+#undef FDCN_SPLIT_UPD_ASM
+#undef FDCN_SPLIT_UPD_OUT
 
 // ---------------------------------------------------------------------------
 // the kernel
@@ -339,14 +422,20 @@ struct KArgs {
 // for LDS (|fm| -> 1).  Bit 1: the single-trade flavour of a W = 1 variant,
 // for batches too small to put a wave on every SIMD: its recurrences run as 4
 // interleaved sub-chains per lane, trading the joins' extra FMAs for in-wave
-// ILP (with one wave on a SIMD nothing else hides the FMA latency).
+// ILP (with one wave on a SIMD nothing else hides the FMA latency).  Bit 2:
+// the paired flavour of a split-form W = 1 variant: two scenarios per wave,
+// 32 lanes each (lanes 0-31 and 32-63), for grids of up to 32 NPT interior
+// nodes -- twice the nodes per lane of the one-scenario variant for the same
+// grid, so the per-step scans, carries and broadcasts are spread over twice
+// as many nodes.  Its per-scenario constants are per-lane values (VGPRs).
 template <int IT, int W, int NPT, int ZG = 0>
 struct Geo {
-  static constexpr int L = 64 * W;
-  static constexpr int SPB = 1;  // one scenario per workgroup (LDS sized per scenario)
+  static constexpr bool kPair = (ZG & 4) != 0;
+  static constexpr int L = kPair ? 32 : 64 * W;  // lanes per scenario
+  static constexpr int SPB = kPair ? 2 : 1;  // scenarios per workgroup (LDS sized per scenario)
   // IT payoff staged in LDS unless it would not fit (8+ waves per scenario)
   static constexpr bool kPhiLds = IT && (W <= 4);
-  static constexpr int kThreads = 64 * W * SPB;
+  static constexpr int kThreads = kPair ? 64 : 64 * W * SPB;
 };
 
 // doubles of LDS per scenario
@@ -372,17 +461,29 @@ __global__ void __launch_bounds__(64 * W)
 fdcn_march(KArgs A) {
   constexpr int L = Geo<IT, W, NPT, ZG>::L;
   constexpr int SPB = Geo<IT, W, NPT, ZG>::SPB;
+  constexpr bool kPair = Geo<IT, W, NPT, ZG>::kPair;
+  static_assert(!kPair || (!IT && W == 1 && split_form(IT, W, NPT) && !(ZG & 3)),
+                "paired flavour: split-form CN, one wave, LDS table");
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  // per-scenario uniform values: SGPRs, or per-lane values when a wave holds
+  // two scenarios
+  auto U = [](double x) __attribute__((always_inline)) { return kPair ? x : uni(x); };
+  auto Ui = [](int x) __attribute__((always_inline)) { return kPair ? x : uni_i(x); };
 
   const int lane = threadIdx.x & 63;
   int lane4 = lane << 2;
   asm volatile("" : "+v"(lane4));  // one VGPR, never rematerialised in the loop
+  const int half = kPair ? lane >> 5 : 0;    // the wave's scenario this lane serves
+  const int hl = kPair ? lane & 31 : lane;   // lane within that scenario
   const int wave_blk = uni_i(threadIdx.x >> 6);
-  const int scen_in_blk = (W == 1) ? wave_blk : 0;
+  const int scen_in_blk = kPair ? half : ((W == 1) ? wave_blk : 0);
   const int wave = (W == 1) ? 0 : wave_blk;  // wave index within the scenario
-  const int scen = uni_i(blockIdx.x * SPB + scen_in_blk);
-  if (scen >= A.B) return;  // whole wave(s) of a missing scenario leave together
-  const int t = wave * 64 + lane;
+  const int scen0 = uni_i(blockIdx.x * SPB + (kPair ? 0 : scen_in_blk));
+  if (scen0 >= A.B) return;  // whole wave(s) of a missing scenario leave together
+  // a paired wave's second scenario may not exist (odd B): its lanes idle
+  const bool valid = !kPair || scen0 + half < A.B;
+  const int scen = kPair ? (valid ? scen0 + half : scen0) : scen0;
+  const int t = wave * 64 + hl;
 
   const int n_nodes = A.n_nodes;
   const int n_int = n_nodes - 2;
@@ -397,11 +498,11 @@ fdcn_march(KArgs A) {
 
   const double* P = A.params + (size_t)scen * FDCN_NPARAM;
   const int32_t* I = A.iparams + (size_t)scen * FDCN_NIPARAM;
-  const double dt = uni(P[FDCN_P_DT]);
-  const double ca = uni(P[FDCN_P_A]);
-  const double cc = uni(P[FDCN_P_C]);
-  const double cbc = uni(P[FDCN_P_BC]);
-  const double tau0 = uni(P[FDCN_P_TAU0]);
+  const double dt = U(P[FDCN_P_DT]);
+  const double ca = U(P[FDCN_P_A]);
+  const double cc = U(P[FDCN_P_C]);
+  const double cbc = U(P[FDCN_P_BC]);
+  const double tau0 = U(P[FDCN_P_TAU0]);
 
   // Dirichlet values of every step, evaluated once up front (while few
   // registers are live) into this wave's workspace row: lane l owns steps
@@ -416,12 +517,14 @@ fdcn_march(KArgs A) {
   double2* bnd = reinterpret_cast<double2*>(A.bnd) +
                  ((size_t)scen * W + wave) *
                      (A.n_pad + kKoRow + (split_form(IT, W, NPT) ? A.n_pad : 0));
-  const int lof = uni_i(I[FDCN_I_LO_FORM]), hif = uni_i(I[FDCN_I_HI_FORM]);
-  const double l0 = uni(P[FDCN_P_LO_C0]), l1 = uni(P[FDCN_P_LO_E0]), l2 = uni(P[FDCN_P_LO_C1]),
-               l3 = uni(P[FDCN_P_LO_E1]);
-  const double h0 = uni(P[FDCN_P_HI_C0]), h1 = uni(P[FDCN_P_HI_E0]), h2 = uni(P[FDCN_P_HI_C1]),
-               h3 = uni(P[FDCN_P_HI_E1]);
-  const int tau_mode = uni_i(I[FDCN_I_TAU_MODE]);
+  const int lof = Ui(I[FDCN_I_LO_FORM]), hif = Ui(I[FDCN_I_HI_FORM]);
+  const double l0 = U(P[FDCN_P_LO_C0]), l1 = U(P[FDCN_P_LO_E0]), l2 = U(P[FDCN_P_LO_C1]),
+               l3 = U(P[FDCN_P_LO_E1]);
+  const double h0 = U(P[FDCN_P_HI_C0]), h1 = U(P[FDCN_P_HI_E0]), h2 = U(P[FDCN_P_HI_C1]),
+               h3 = U(P[FDCN_P_HI_E1]);
+  const int tau_mode = Ui(I[FDCN_I_TAU_MODE]);
+  // steps m = hl (mod L) are this lane's (kStride lanes per scenario)
+  constexpr int kStride = kPair ? 32 : 64;
   double tau_end = tau0 + (double)A.n_time * dt;  // tau after the last step
   if (tau_mode == 1) {
     // (tau_{m+1}, tau_m) of every step into the owner lane's workspace slot
@@ -429,11 +532,12 @@ fdcn_march(KArgs A) {
     double tc = tau0;
     int kc = 0;
     TauRun run;
-    while (tau_next_run(tc, kc, A.n_pad, dt, run)) {  // wave-uniform
+    while (tau_next_run(tc, kc, A.n_pad, dt, run)) {  // uniform per scenario
       if (run.k < A.n_time && A.n_time <= run.k + run.len)
         tau_end = (A.n_time == run.k + run.len)
                       ? run.t_next : run.t + (double)(A.n_time - run.k) * run.delta;
-      for (int m = run.k + ((lane - run.k) & 63); m < run.k + run.len; m += 64) {
+      for (int m = run.k + ((hl - run.k) & (kStride - 1)); m < run.k + run.len && valid;
+           m += kStride) {
         const int j = m - run.k;
         const double tp = run.t + (double)j * run.delta;
         const double tn = (j + 1 == run.len) ? run.t_next : run.t + (double)(j + 1) * run.delta;
@@ -447,15 +551,16 @@ fdcn_march(KArgs A) {
   // expression and operand order of the in-loop form it replaces (bitwise the
   // same numbers).  A knock-out that removes node 0 or the last node sets
   // lo_prev / hi_prev to the rebate instead: the step after one recomputes
-  // its term from the raw values, kept in a second table (bnd_raw).
+  // its term from the raw values, kept in a second table (bnd_raw; evaluating
+  // them again in the loop would keep exp's registers live in the march).
   constexpr bool kTabSplit = split_form(IT, W, NPT);
   double2* bnd_raw = bnd + A.n_pad + kKoRow;  // kTabSplit only
   (void)bnd_raw;
   {
     const double* vb = A.v_init + (size_t)scen * n_nodes;
-    const double v_lo0 = (IT || kTabSplit) ? uni(vb[0]) : 0.0;
-    const double v_hi0 = (IT || kTabSplit) ? uni(vb[n_nodes - 1]) : 0.0;
-    for (int m = lane; m < A.n_pad; m += 64) {
+    const double v_lo0 = (IT || kTabSplit) ? U(vb[0]) : 0.0;
+    const double v_hi0 = (IT || kTabSplit) ? U(vb[n_nodes - 1]) : 0.0;
+    for (int m = hl; m < A.n_pad && valid; m += kStride) {
       double tau = tau0 + (double)(m + 1) * dt, tp = tau0 + (double)m * dt;
       if (tau_mode == 1) {
         const double2 tt = bnd[m];
@@ -488,11 +593,11 @@ fdcn_march(KArgs A) {
   // lane geometry
   const int L_act = (n_int + NPT - 1) / NPT;
   const int L_short = L_act * NPT - n_int;
-  const bool active = t < L_act;
+  const bool active = t < L_act && valid;
   const bool shrt = t < L_short;
   // 1.0 on the lane that holds interior node 0 / the last interior node
-  const double e_first = (t == 0) ? 1.0 : 0.0;
-  const double e_last = (t == L_act - 1) ? 1.0 : 0.0;
+  const double e_first = (t == 0 && valid) ? 1.0 : 0.0;
+  const double e_last = (t == L_act - 1 && valid) ? 1.0 : 0.0;
   (void)e_first;
   (void)e_last;
   const int s_t = t * NPT - (t < L_short ? t : L_short);  // first interior index
@@ -526,6 +631,10 @@ fdcn_march(KArgs A) {
   // The phantom slot's pass-2 multiplier mlast2 (0 on short lanes) writes
   // the phantom's zero rhs instead of the passed-through value.
   double fm_act = 0.0, fmM_act = 0.0, mlast2 = 0.0;
+  // glast2: the backward carry multiplier of the chunk's last node, 0 on the
+  // last lane of a paired wave's first scenario (its neighbour lane belongs
+  // to the other scenario); glast elsewhere
+  double glast2 = 0.0;
   double mulLF = 0.0, mulLB = 0.0;  // products across the last sub-chain
   double fmM = 0.0, bmM = 0.0;      // products across a full sub-chain
   int nst_f = 6, nst_b = 6;         // scan stages that carry weight above 1e-18
@@ -573,10 +682,12 @@ fdcn_march(KArgs A) {
     mlast = shrt ? 1.0 : p.fm;
     glast = shrt ? 1.0 : p.bm;
     mlast2 = shrt ? 0.0 : p.fm;
-    fm_act = active ? p.fm : 0.0;
+    glast2 = (kPair && hl == 31) ? 0.0 : glast;
+    // kPair: lane 32 also drops the forward carry it receives from lane 31
+    fm_act = (active && !(kPair && hl == 0)) ? p.fm : 0.0;
     const double fM1 = pow_n<NPT>(p.fm, M - 1), bM1 = pow_n<NPT>(p.bm, M - 1);
-    fmM = uni(fM1 * p.fm);
-    bmM = uni(bM1 * p.bm);
+    fmM = U(fM1 * p.fm);
+    bmM = U(bM1 * p.bm);
     mulLF = shrt ? fM1 : fmM;
     fmM_act = active ? fmM : 0.0;
     mulLB = shrt ? bM1 : bmM;
@@ -588,12 +699,13 @@ fdcn_march(KArgs A) {
       const int d = 1 << j;
       // zero where the shuffle source lane does not exist: the scan step
       // b += FW*b_src then needs no lane mask
-      FW[j] = (lane >= d) ? f : 0.0;
-      GW[j] = (lane + d < 64) ? g : 0.0;
+      // (kPair: lanes of the other scenario count as missing sources)
+      FW[j] = (hl >= d) ? f : 0.0;
+      GW[j] = (hl + d < kStride) ? g : 0.0;
       const double fo = shfl_up1(f, d);
       const double go = shfl_dn1(g, d);
-      f = (lane >= d) ? f * fo : f;
-      g = (lane + d < 64) ? g * go : g;
+      f = (hl >= d) ? f * fo : f;
+      g = (hl + d < kStride) ? g * go : g;
     }
     Fpre = f;
     Gsuf = g;
@@ -604,11 +716,12 @@ fdcn_march(KArgs A) {
     // rounding (the same criterion as the Sherman-Morrison extent).
     {
       double qf = fabs(pow_n<NPT>(p.fm, NPT - 1)), qb = fabs(pow_n<NPT>(p.bm, NPT - 1));
+      constexpr int kMaxSt = kPair ? 5 : 6;
       int nf = 0, nb = 0;
-      while (nf < 6 && qf > 1e-18) { qf *= qf; ++nf; }
-      while (nb < 6 && qb > 1e-18) { qb *= qb; ++nb; }
-      nst_f = uni_i(nf);
-      nst_b = uni_i(nb);
+      while (nf < kMaxSt && qf > 1e-18) { qf *= qf; ++nf; }
+      while (nb < kMaxSt && qb > 1e-18) { qb *= qb; ++nb; }
+      nst_f = kPair ? umax_halves(nf) : uni_i(nf);
+      nst_b = kPair ? umax_halves(nb) : uni_i(nb);
     }
     if constexpr (W > 1) {
       if (lane == 63) xch[Xch<W>::kFtot + wave] = Fpre;
@@ -795,7 +908,9 @@ fdcn_march(KArgs A) {
           const int k = j * M + i;
           const double yn = (i == M - 1) ? c[j] : Wr(k + 1);
           if (k == NPT - 1)
-            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(Wr(k)) : "v"(glast), "v"(yn));
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(Wr(k)) : "v"(glast2), "v"(yn));
+          else if constexpr (kPair)
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(Wr(k)) : "v"(bm), "v"(yn));
           else
             asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(Wr(k)) : "s"(bm), "v"(yn));
         }
@@ -829,7 +944,9 @@ fdcn_march(KArgs A) {
 
   // broadcast of the solution at interior node 0 (lane 0 of wave 0)
   auto bcast_first = [&](double v0lane) __attribute__((always_inline)) -> double {
-    if constexpr (W == 1) {
+    if constexpr (kPair) {  // lane 0 / lane 32: each scenario's own node 0
+      return half ? read_lane(v0lane, 32) : read_lane(v0lane, 0);
+    } else if constexpr (W == 1) {
       return read_lane(v0lane, 0);
     } else {
       if (t == 0) xch[Xch<W>::kY0] = v0lane;
@@ -861,7 +978,7 @@ fdcn_march(KArgs A) {
         ztab[(tab * lz + t) * (NPT + 1) + k] = (k == NPT - 1 && shrt) ? 0.0 : Out(k);
     }
     const double z0 = bcast_first(Out(0));
-    return uni(p.kappa / (1.0 + p.kappa * z0));
+    return U(p.kappa / (1.0 + p.kappa * z0));
   };
 
   const bool use_r = A.n_ranna > 0;
@@ -869,13 +986,13 @@ fdcn_march(KArgs A) {
   int kext = 1;
   double smc_r = 0.0, smc_c = 0.0;
   if (use_c) {
-    ph = make_phase(0.5, dt, ca, cc, cbc);
+    ph = make_phase<kPair>(0.5, dt, ca, cc, cbc);
     setup_scan(ph);
     smc_c = build_sm(ph, 1);
     kext = max(kext, sm_extent(ph.fm, n_int));
   }
   if (use_r) {
-    ph = make_phase(1.0, dt, ca, cc, cbc);
+    ph = make_phase<kPair>(1.0, dt, ca, cc, cbc);
     setup_scan(ph);
     smc_r = build_sm(ph, 0);
     kext = max(kext, sm_extent(ph.fm, n_int));
@@ -887,8 +1004,8 @@ fdcn_march(KArgs A) {
 
   // ---- load state -------------------------------------------------------
   const double* vin = A.v_init + (size_t)scen * n_nodes;
-  double V0 = uni(vin[0]);
-  double VN = uni(vin[n_nodes - 1]);
+  double V0 = U(vin[0]);
+  double VN = U(vin[n_nodes - 1]);
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     const int node = s_t + 1 + k;
@@ -908,56 +1025,97 @@ fdcn_march(KArgs A) {
       QS[k] = A.n_ranna > 0 ? 0.0 : V[k];
     }
   }
-  const int ko_lo = uni_i(I[FDCN_I_KO_LO]);
-  const int ko_hi = uni_i(I[FDCN_I_KO_HI]);
+  const int ko_lo = Ui(I[FDCN_I_KO_LO]);
+  const int ko_hi = Ui(I[FDCN_I_KO_HI]);
   // knock-out masks of this wave (interior nodes j <= ko_lo or j >= ko_hi),
   // computed once: lanes are ordered by node, so the knocked-out lanes of
-  // each side are a contiguous run plus at most one partial lane
+  // each side are a contiguous run plus at most one partial lane.  A paired
+  // wave has one set per scenario (kml/kmh: lanes 0-31, kml2/kmh2: 32-63).
   KoMask kml{0ull, 0ull, 0, -1}, kmh{0ull, 0ull, 0, -1};
+  KoMask kml2{0ull, 0ull, 0, -1}, kmh2{0ull, 0ull, 0, -1};
+  (void)kml2;
+  (void)kmh2;
   if constexpr (!IT) {
     const unsigned long long act =
         __builtin_amdgcn_read_exec() & (unsigned long long)__ballot(active);
-    const int base = wave * 64;
-    if (ko_lo >= 1) {  // interior indices 0 .. ko_lo-1 are out
-      int tl, sl;
-      if (ko_lo >= n_int) { tl = L_act; sl = 0; }
-      else lane_slot<NPT>(ko_lo - 1, L_short, tl, sl);
-      // lanes < tl fully out; lane tl out for slots <= sl
-      const int rl = tl - base;
-      kml.full = rl <= 0 ? 0ull : (rl >= 64 ? ~0ull : ((1ull << rl) - 1ull));
-      kml.full &= act;
-      if (ko_lo < n_int && rl >= 0 && rl < 64) { kml.part = 1ull << rl; kml.k0 = 0; kml.k1 = sl; }
-    }
-    if (ko_hi <= n_int) {  // interior indices ko_hi-1 .. n_int-1 are out
-      int th, sh;
-      if (ko_hi <= 1) { th = 0; sh = 0; }
-      else lane_slot<NPT>(ko_hi - 1, L_short, th, sh);
-      // lane th out for slots >= sh; lanes > th fully out
-      const int rh = th - base;
-      kmh.full = rh >= 63 ? 0ull : (rh < 0 ? ~0ull : ~((2ull << rh) - 1ull));
-      kmh.full &= act;
-      if (rh >= 0 && rh < 64) { kmh.part = 1ull << rh; kmh.k0 = sh; kmh.k1 = NPT - 1; }
+    // one scenario's masks: its lanes are bits b0 .. b0+nl-1 of the wave,
+    // lane t of the scenario is bit b0 + t - base
+    auto masks = [&](int klo, int khi, int base, int b0, int nl, KoMask& ml, KoMask& mh)
+        __attribute__((always_inline)) {
+      const unsigned long long all = (nl >= 64 ? ~0ull : ((1ull << nl) - 1ull)) << b0;
+      if (klo >= 1) {  // interior indices 0 .. klo-1 are out
+        int tl, sl;
+        if (klo >= n_int) { tl = L_act; sl = 0; }
+        else lane_slot<NPT>(klo - 1, L_short, tl, sl);
+        // lanes < tl fully out; lane tl out for slots <= sl
+        const int rl = tl - base;
+        ml.full = rl <= 0 ? 0ull : (rl >= nl ? all : (((1ull << rl) - 1ull) << b0));
+        ml.full &= act;
+        if (klo < n_int && rl >= 0 && rl < nl) { ml.part = act & (1ull << (b0 + rl)); ml.k0 = 0; ml.k1 = sl; }
+      }
+      if (khi <= n_int) {  // interior indices khi-1 .. n_int-1 are out
+        int th, sh;
+        if (khi <= 1) { th = 0; sh = 0; }
+        else lane_slot<NPT>(khi - 1, L_short, th, sh);
+        // lane th out for slots >= sh; lanes > th fully out
+        const int rh = th - base;
+        mh.full = rh >= nl - 1 ? 0ull : (rh < 0 ? all : (all & ~(((2ull << rh) - 1ull) << b0)));
+        mh.full &= act;
+        if (rh >= 0 && rh < nl) { mh.part = act & (1ull << (b0 + rh)); mh.k0 = sh; mh.k1 = NPT - 1; }
+      }
+    };
+    if constexpr (kPair) {
+      masks(__builtin_amdgcn_readlane(ko_lo, 0), __builtin_amdgcn_readlane(ko_hi, 0), 0, 0, 32,
+            kml, kmh);
+      masks(__builtin_amdgcn_readlane(ko_lo, 32), __builtin_amdgcn_readlane(ko_hi, 32), 0, 32, 32,
+            kml2, kmh2);
+    } else {
+      masks(ko_lo, ko_hi, wave * 64, 0, 64, kml, kmh);
     }
   }
   const unsigned long long shrt_ballot = kSplit ? (unsigned long long)__ballot(shrt) : 0ull;
   (void)shrt_ballot;
   unsigned long long kom_addr = 0;  // this wave's mask row (KoLoad variants)
-  if constexpr (KoLoad<IT, NPT>::value) {
+  unsigned long long kom_addr2 = 0, kom_addr12 = 0;  // kPair: second scenario's / both
+  if constexpr (KoLoad<IT, NPT, ZG>::value) {
     unsigned long long* kom = reinterpret_cast<unsigned long long*>(bnd + A.n_pad);
-    // kRec keeps the phantom slot of short lanes at zero: never knock it out
-    const unsigned long long shrt_lanes = kRec ? (unsigned long long)__ballot(shrt) : 0ull;
-    if (lane < NPT) {
-      const int k = lane;
-      unsigned long long mk = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) |
-                              kmh.full | ((k >= kmh.k0 && k <= kmh.k1) ? kmh.part : 0ull);
-      if (k == NPT - 1) mk &= ~shrt_lanes;
-      kom[k] = mk;
+    // kRec / kSplit keep the phantom slot of short lanes at zero: never knock it out
+    const unsigned long long shrt_lanes = (kRec || kSplit) ? (unsigned long long)__ballot(shrt) : 0ull;
+    auto slot_mask = [&](const KoMask& ml, const KoMask& mh, int k) {
+      unsigned long long mk = ml.full | ((k >= ml.k0 && k <= ml.k1) ? ml.part : 0ull) | mh.full |
+                              ((k >= mh.k0 && k <= mh.k1) ? mh.part : 0ull);
+      return k == NPT - 1 ? (mk & ~shrt_lanes) : mk;
+    };
+    if constexpr (kPair) {
+      // rows: the first scenario's [0, NPT) its own masks, [32, 32 + NPT) both
+      // scenarios'; the second scenario's [0, NPT) its own (each lane writes
+      // into its own scenario's row)
+      if (hl < NPT && valid) {
+        const int k = hl;
+        kom[k] = half ? slot_mask(kml2, kmh2, k) : slot_mask(kml, kmh, k);
+        if (!half) kom[32 + k] = slot_mask(kml, kmh, k) | slot_mask(kml2, kmh2, k);
+      }
+    } else if (lane < NPT) {
+      kom[lane] = slot_mask(kml, kmh, lane);
     }
     // the loop reads the row back with s_load from inline asm, which the
     // compiler's wait-count tracking does not see: drain the stores here
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    kom_addr = (unsigned long long)kom;
+    const unsigned long long ka = (unsigned long long)kom;
+    if constexpr (kPair) {
+      const unsigned lo0 = __builtin_amdgcn_readlane((unsigned)ka, 0);
+      const unsigned hi0 = __builtin_amdgcn_readlane((unsigned)(ka >> 32), 0);
+      const unsigned lo1 = __builtin_amdgcn_readlane((unsigned)ka, 32);
+      const unsigned hi1 = __builtin_amdgcn_readlane((unsigned)(ka >> 32), 32);
+      kom_addr = ((unsigned long long)hi0 << 32) | lo0;
+      kom_addr2 = ((unsigned long long)hi1 << 32) | lo1;
+      kom_addr12 = kom_addr + 32 * sizeof(unsigned long long);
+    } else {
+      kom_addr = ka;
+    }
   }
+  (void)kom_addr2;
+  (void)kom_addr12;
   (void)kom_addr;
   // every lane that holds a Sherman-Morrison table row is fully inside the
   // lower knock-out region (sm_skip below)
@@ -967,21 +1125,21 @@ fdcn_march(KArgs A) {
     sm_covered = (kml.full & lzm) == lzm;
   }
   (void)sm_covered;
-  int mpos = uni_i(I[FDCN_I_MON_START]);
-  const int mend = mpos + uni_i(I[FDCN_I_MON_COUNT]);
-  // entries < 1 never match a step: skip them (the oracle's `while` does)
-  if (!IT)
-    while (mpos < mend && uni_i(A.mon_step[mpos]) < 1) ++mpos;
-  // monitor entry mpos (step, rebate) and the next one, loaded a monitor
-  // step ahead of their use so the scalar-load latency is off the step
-  int next_mon = 0x7fffffff, pf_mon = 0x7fffffff;
-  double cur_reb = 0.0, pf_reb = 0.0;
-  if (!IT && mpos < mend) {
-    next_mon = uni_i(A.mon_step[mpos]);
-    cur_reb = uni(A.mon_rebate[mpos]);
-    if (mpos + 1 < mend) {
-      pf_mon = uni_i(A.mon_step[mpos + 1]);
-      pf_reb = uni(A.mon_rebate[mpos + 1]);
+  // monitoring entries: one run per scenario of the wave (mon2: a paired
+  // wave's second scenario; an odd batch's missing one has none)
+  MonRun mon, mon2;
+  mon.init(A.mon_step, A.mon_rebate, 0, 0);
+  mon2.init(A.mon_step, A.mon_rebate, 0, 0);
+  if constexpr (!IT) {
+    const int ms = Ui(I[FDCN_I_MON_START]), mc = Ui(I[FDCN_I_MON_COUNT]);
+    if constexpr (kPair) {
+      mon.init(A.mon_step, A.mon_rebate, __builtin_amdgcn_readlane(ms, 0),
+               __builtin_amdgcn_readlane(mc, 0));
+      if (scen0 + 1 < A.B)
+        mon2.init(A.mon_step, A.mon_rebate, __builtin_amdgcn_readlane(ms, 32),
+                  __builtin_amdgcn_readlane(mc, 32));
+    } else {
+      mon.init(A.mon_step, A.mon_rebate, ms, mc);
     }
   }
 
@@ -1003,7 +1161,7 @@ fdcn_march(KArgs A) {
     smc = smc_r;
     tab = 0;
   } else {
-    ph = make_phase(0.5, dt, ca, cc, cbc);
+    ph = make_phase<kPair>(0.5, dt, ca, cc, cbc);
     setup_scan(ph);
     smc = smc_c;
     tab = 1;
@@ -1012,7 +1170,7 @@ fdcn_march(KArgs A) {
   s_l = shrt ? 0.0 : ph.s;
 
   double2 bnd_cur = make_double2(0.0, 0.0);
-  double2 bnd_nxt = bnd[lane];  // steps 0..63
+  double2 bnd_nxt = bnd[hl];  // steps 0..kStride-1
   int ko_prev = 0;  // kSplit: bit 0 / 1 -- the last step knocked out node 0 / the last node
   (void)ko_prev;
   double halo_l = 0.0, halo_r = 0.0;
@@ -1022,19 +1180,29 @@ fdcn_march(KArgs A) {
   }
   for (int m = 0; m < A.n_time; ++m) {
     if (m == A.n_ranna && use_r) {  // Rannacher -> Crank-Nicolson
-      ph = make_phase(0.5, dt, ca, cc, cbc);
+      if constexpr (kPair) {
+        // reloaded rather than kept live through the march (VGPRs, per lane)
+        const double* Pr = P;
+        asm volatile("" : "+v"(Pr));
+        ph = make_phase<kPair>(0.5, Pr[FDCN_P_DT], Pr[FDCN_P_A], Pr[FDCN_P_C], Pr[FDCN_P_BC]);
+      } else {
+        ph = make_phase<kPair>(0.5, dt, ca, cc, cbc);
+      }
       setup_scan(ph);
       smc = smc_c;
       smc_l = sm_row * smc;
       s_l = shrt ? 0.0 : ph.s;
       tab = 1;
     }
-    if ((m & 63) == 0) {  // Dirichlet values of the next 64 steps, one per lane
+    if ((m & (kStride - 1)) == 0) {  // Dirichlet values of the next steps, one per lane
       bnd_cur = bnd_nxt;
-      if (m + 64 < A.n_pad) bnd_nxt = bnd[m + 64 + lane];  // prefetch the block after
+      if (m + kStride < A.n_pad) bnd_nxt = bnd[m + kStride + hl];  // prefetch the block after
     }
-    double lo_new = read_lane(bnd_cur.x, m & 63);  // kSplit: the tabulated rhs terms
-    double hi_new = read_lane(bnd_cur.y, m & 63);
+    // kSplit: the tabulated rhs terms; kPair: each scenario's from its own lanes
+    double lo_new = kPair ? (half ? read_lane(bnd_cur.x, 32 + (m & 31)) : read_lane(bnd_cur.x, m & 31))
+                          : read_lane(bnd_cur.x, m & 63);
+    double hi_new = kPair ? (half ? read_lane(bnd_cur.y, 32 + (m & 31)) : read_lane(bnd_cur.y, m & 31))
+                          : read_lane(bnd_cur.y, m & 63);
 
     // ---- 1. rhs ------------------------------------------------------------
     if constexpr (IT) {
@@ -1060,9 +1228,11 @@ fdcn_march(KArgs A) {
       // writes T, and x = (r u)/(theta r) - c2 V afterwards.
       double blo = lo_new, bhi = hi_new;
       if (ko_prev) {  // after a knock-out step: terms from the rebate (uniform branch)
-        const double2 raw = bnd_raw[m];
-        if (ko_prev & 1) blo = ph.th * (ph.pl * fma(ph.c2, V0, uni(raw.x)));
-        if (ko_prev & 2) bhi = ph.th * (ph.pu * fma(ph.c2, VN, uni(raw.y)));
+        const int kb = kPair ? ((ko_prev >> (2 * half)) & 3) : ko_prev;
+        const double2 raw = bnd_raw[m];  // the step's raw Dirichlet values
+        const double rlo = U(raw.x), rhi = U(raw.y);
+        if (kb & 1) blo = ph.th * (ph.pl * fma(ph.c2, V0, rlo));
+        if (kb & 2) bhi = ph.th * (ph.pu * fma(ph.c2, VN, rhi));
         ko_prev = 0;
       }
       vb0 = fma(e_first, blo, V[0]);
@@ -1184,7 +1354,9 @@ fdcn_march(KArgs A) {
     int zoff = 0;
     if (do_sm) {
       double y0;
-      if constexpr (kRec) {
+      if constexpr (kPair) {
+        y0 = bcast_first(Out(0));
+      } else if constexpr (kRec) {
         y0 = read_lane(y0c, 0);
       } else if constexpr (W == 1) {
         y0 = read_lane(Out(0), 0);
@@ -1214,7 +1386,7 @@ fdcn_march(KArgs A) {
     // kRec: the correction only changes nodes of lanes < lz; on a knock-out
     // step whose lower side removes all of them the projection overwrites it
     // with the rebate, so it is skipped (config 5 knocks out on every step)
-    const bool sm_skip = kRec && sm_covered && (m + 1 == next_mon);
+    const bool sm_skip = kRec && sm_covered && (m + 1 == mon.next);
     if (!sm_skip) {
       const int poff = opaque(kPhiLds ? t : s_t + 1);
       auto phi_at = [&](int k) -> double {
@@ -1246,34 +1418,14 @@ fdcn_march(KArgs A) {
           }
         }
         if constexpr (kSplit) {
-          if (k + 4 < NPT) {
-            asm volatile(
-                "v_fma_f64 %4, %8, %9, %4\n\t"
-                "v_fma_f64 %5, %8, %10, %5\n\t"
-                "v_fma_f64 %6, %8, %11, %6\n\t"
-                "v_fma_f64 %7, %8, %12, %7\n\t"
-                "v_fma_f64 %0, %13, %4, -%0\n\t"
-                "v_fma_f64 %1, %13, %5, -%1\n\t"
-                "v_fma_f64 %2, %13, %6, -%2\n\t"
-                "v_fma_f64 %3, %13, %7, -%3"
-                : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(T[k]),
-                  "+v"(T[k + 1]), "+v"(T[k + 2]), "+v"(T[k + 3])
-                : "v"(g), "v"(zk[0]), "v"(zk[1]), "v"(zk[2]), "v"(zk[3]), "s"(ph.s));
-          } else {
-            // the last slot takes s_l (0 on short lanes): the phantom stays zero
-            asm volatile(
-                "v_fma_f64 %4, %8, %9, %4\n\t"
-                "v_fma_f64 %5, %8, %10, %5\n\t"
-                "v_fma_f64 %6, %8, %11, %6\n\t"
-                "v_fma_f64 %7, %8, %12, %7\n\t"
-                "v_fma_f64 %0, %13, %4, -%0\n\t"
-                "v_fma_f64 %1, %13, %5, -%1\n\t"
-                "v_fma_f64 %2, %13, %6, -%2\n\t"
-                "v_fma_f64 %3, %14, %7, -%3"
-                : "+v"(V[k]), "+v"(V[k + 1]), "+v"(V[k + 2]), "+v"(V[k + 3]), "+v"(T[k]),
-                  "+v"(T[k + 1]), "+v"(T[k + 2]), "+v"(T[k + 3])
-                : "v"(g), "v"(zk[0]), "v"(zk[1]), "v"(zk[2]), "v"(zk[3]), "s"(ph.s), "v"(s_l));
-          }
+          // T += g z; V = s T - V (the last slot with s_l: 0 on short lanes,
+          // so the phantom stays zero); kPair: s is a per-lane value
+          if (k + 4 < NPT)
+            split_update<kPair, false>(V[k], V[k + 1], V[k + 2], V[k + 3], T[k], T[k + 1],
+                                       T[k + 2], T[k + 3], g, zk, ph.s, s_l);
+          else
+            split_update<kPair, true>(V[k], V[k + 1], V[k + 2], V[k + 3], T[k], T[k + 1],
+                                      T[k + 2], T[k + 3], g, zk, ph.s, s_l);
         } else if constexpr (kRec) {
           // V holds s u already (both phases): x = s u + (s g) z
 #pragma unroll
@@ -1320,8 +1472,10 @@ fdcn_march(KArgs A) {
       V0 = lo_new;
       VN = hi_new;
     }
-    if (!IT && m + 1 == next_mon) {  // knock-out projection (uniform branch)
-      const double reb = cur_reb;
+    const bool hit1 = !IT && m + 1 == mon.next;
+    const bool hit2 = kPair && m + 1 == mon2.next;  // a paired wave's second scenario
+    if (hit1 || hit2) {  // knock-out projection (uniform branch)
+      const double reb = kPair ? (half ? mon2.cur : mon.cur) : mon.cur;
       double rebv = reb;  // VGPR copy: v_cndmask takes the mask as its SGPR operand
       asm volatile("" : "+v"(rebv));
       // NPT <= 40: the per-slot masks are loop-invariant, the compiler
@@ -1331,7 +1485,7 @@ fdcn_march(KArgs A) {
       // exec-masked v_mov_b64 per slot (config 5: 29.3 -> 26.0 ms per
       // launch).  Rebuilding the masks on the scalar unit from (full, part,
       // k0, k1) measured slower still (34.8 ms): five SALU per slot.
-      if constexpr (KoLoad<IT, NPT>::value) {
+      if constexpr (KoLoad<IT, NPT, ZG>::value) {
         // eight slots per block: each slot is one v_mov_b64 of the rebate
         // under an exec mask set on the scalar unit (s_and_b64 with the
         // saved exec), while the next block's eight masks arrive (one
@@ -1339,7 +1493,7 @@ fdcn_march(KArgs A) {
         // output is valid on exit; exec is restored inside the block)
         // (laundered so the compiler cannot hoist the eight block
         // addresses out of the time loop and spill them)
-        unsigned long long ka = kom_addr;
+        unsigned long long ka = kPair ? (hit1 ? (hit2 ? kom_addr12 : kom_addr) : kom_addr2) : kom_addr;
         asm volatile("" : "+s"(ka));
         KoMask16 mcur;
         asm volatile("s_load_dwordx16 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)"
@@ -1385,8 +1539,13 @@ fdcn_march(KArgs A) {
       } else {
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
-        unsigned long long mk = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) |
-                                kmh.full | ((k >= kmh.k0 && k <= kmh.k1) ? kmh.part : 0ull);
+        unsigned long long mk = 0ull;
+        if (hit1)
+          mk = kml.full | ((k >= kml.k0 && k <= kml.k1) ? kml.part : 0ull) | kmh.full |
+               ((k >= kmh.k0 && k <= kmh.k1) ? kmh.part : 0ull);
+        if (kPair && hit2)
+          mk |= kml2.full | ((k >= kml2.k0 && k <= kml2.k1) ? kml2.part : 0ull) | kmh2.full |
+                ((k >= kmh2.k0 && k <= kmh2.k1) ? kmh2.part : 0ull);
         if (kSplit && k == NPT - 1) mk &= ~shrt_ballot;  // the phantom stays zero
         unsigned lo = (unsigned)__double_as_longlong(V[k]);
         unsigned hi = (unsigned)(__double_as_longlong(V[k]) >> 32);
@@ -1399,24 +1558,22 @@ fdcn_march(KArgs A) {
         V[k] = __longlong_as_double(((long long)hi << 32) | lo);
       }
       }
-      if (0 <= ko_lo) V0 = reb;
-      if (n_nodes - 1 >= ko_hi) VN = reb;
-      if constexpr (kSplit) ko_prev = (0 <= ko_lo ? 1 : 0) | (n_nodes - 1 >= ko_hi ? 2 : 0);
-      // advance to the prefetched entry; request the one after it
-      ++mpos;
-      next_mon = mpos < mend ? pf_mon : 0x7fffffff;
-      cur_reb = pf_reb;
-      if (mpos + 1 < mend) {
-        pf_mon = uni_i(A.mon_step[mpos + 1]);
-        pf_reb = uni(A.mon_rebate[mpos + 1]);
+      const bool hit_me = kPair ? (half ? hit2 : hit1) : true;
+      if (hit_me && 0 <= ko_lo) V0 = reb;
+      if (hit_me && n_nodes - 1 >= ko_hi) VN = reb;
+      if constexpr (kSplit) {
+        // which boundary nodes the knock-out removed, per scenario (uniform)
+        auto kbits = [&](int klo, int khi) { return (0 <= klo ? 1 : 0) | (n_nodes - 1 >= khi ? 2 : 0); };
+        if constexpr (kPair)
+          ko_prev = (hit1 ? kbits(__builtin_amdgcn_readlane(ko_lo, 0),
+                                  __builtin_amdgcn_readlane(ko_hi, 0)) : 0) |
+                    (hit2 ? kbits(__builtin_amdgcn_readlane(ko_lo, 32),
+                                  __builtin_amdgcn_readlane(ko_hi, 32)) << 2 : 0);
+        else
+          ko_prev = kbits(ko_lo, ko_hi);
       }
-      if (next_mon <= m + 1) {  // entries not strictly increasing: skip (slow path)
-        while (mpos < mend && uni_i(A.mon_step[mpos]) <= m + 1) ++mpos;
-        next_mon = (mpos < mend) ? uni_i(A.mon_step[mpos]) : 0x7fffffff;
-        cur_reb = (mpos < mend) ? uni(A.mon_rebate[mpos]) : 0.0;
-        pf_mon = (mpos + 1 < mend) ? uni_i(A.mon_step[mpos + 1]) : 0x7fffffff;
-        pf_reb = (mpos + 1 < mend) ? uni(A.mon_rebate[mpos + 1]) : 0.0;
-      }
+      if (hit1) mon.advance(A.mon_step, A.mon_rebate, m + 1);
+      if (kPair && hit2) mon2.advance(A.mon_step, A.mon_rebate, m + 1);
     }
     if constexpr (kNatural) {
       // pointwise rhs: no halos
@@ -1436,9 +1593,13 @@ fdcn_march(KArgs A) {
     }
   }
   if constexpr (kSplit) {  // likewise, unless the last step knocked the node out
+    // (the last step's raw values from the table: the loop keeps no Dirichlet
+    // coefficients live)
     if (A.n_time > 0) {
-      if (!(ko_prev & 1)) V0 = bnd_eval(lof, l0, l1, l2, l3, tau_end);
-      if (!(ko_prev & 2)) VN = bnd_eval(hif, h0, h1, h2, h3, tau_end);
+      const double2 raw = bnd_raw[A.n_time - 1];
+      const int kb = kPair ? ((ko_prev >> (2 * half)) & 3) : ko_prev;
+      if (!(kb & 1)) V0 = U(raw.x);
+      if (!(kb & 2)) VN = U(raw.y);
     }
   }
   // ---- store ---------------------------------------------------------------
@@ -1451,7 +1612,7 @@ fdcn_march(KArgs A) {
       if (k < NPT - 1 || !shrt) vout[node] = overflow ? poison : V[k];
     }
   }
-  if (t == 0) {
+  if (t == 0 && valid) {
     vout[0] = overflow ? poison : V0;
     vout[n_nodes - 1] = overflow ? poison : VN;
   }
@@ -1488,12 +1649,14 @@ struct Variant {
   int (*lds_per_scen)(int lz);  // the kernel's own LDS layout, in doubles
   int zg;                       // correction table in the workspace
   int lat;                      // single-trade (in-wave ILP) flavour
+  int pair;                     // two scenarios per wave (32 lanes each)
 };
 
 template <int IT, int W, int NPT, int ZG = 0>
 Variant mk() {
   return Variant{IT, W, NPT, &fdcn_march<IT, W, NPT, ZG>, Geo<IT, W, NPT, ZG>::kThreads,
-                 Geo<IT, W, NPT, ZG>::SPB, &lds_doubles_per_scen<IT, W, NPT, ZG>, ZG & 1, ZG >> 1};
+                 Geo<IT, W, NPT, ZG>::SPB, &lds_doubles_per_scen<IT, W, NPT, ZG>, ZG & 1,
+                 (ZG >> 1) & 1, (ZG >> 2) & 1};
 }
 
 // W=1: throughput (one wavefront per scenario).  W>1: grids beyond 64*64
@@ -1508,7 +1671,14 @@ Variant mk() {
       mk<IT, 8, 40, 1>(), mk<IT, 16, 40, 1>(), mk<IT, 1, 8, 2>(), mk<IT, 1, 16, 2>(),       \
       mk<IT, 1, 32, 2>()
 
-const Variant kVariants[] = {FDCN_VARIANTS(0), FDCN_VARIANTS(1)};
+// The paired flavour (CN split form) for grids of up to 256 interior nodes,
+// against one scenario per wave at 4 nodes per lane.  Measured on the
+// config-3 batch (10 000 scenarios x 2000 steps, tools/gpu_pair_ab.sh):
+// 256 nodes 3.26 -> 2.94 ms; but 512 nodes 4.35 -> 4.96 (NPT 8 vs paired
+// 16) and 1024 nodes 5.81 -> 6.76 (NPT 16 vs paired 32): the paired waves'
+// per-lane constants push them to 176 / 242 VGPRs, two waves per SIMD where
+// the one-scenario variants keep three, so only the shortest chunks gain.
+const Variant kVariants[] = {FDCN_VARIANTS(0), mk<0, 1, 8, 4>(), FDCN_VARIANTS(1)};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 // Lanes whose chunks must hold the Sherman-Morrison table to cover k_cap nodes.
@@ -1530,7 +1700,8 @@ constexpr size_t kLdsLimit = 160 * 1024;
 bool fits(const Variant& v, int n_int, int k_cap, bool no_idle_wave = true) {
   const int L_act = (n_int + v.npt - 1) / v.npt;
   const int L_short = L_act * v.npt - n_int;
-  if (L_act > 64 * v.w || L_short >= L_act || v.npt > n_int) return false;
+  const int lanes = v.pair ? 32 : 64 * v.w;  // lanes per scenario
+  if (L_act > lanes || L_short >= L_act || v.npt > n_int) return false;
   if (no_idle_wave && L_act <= 64 * (v.w - 1)) return false;
   const int kc = k_cap > 0 ? k_cap : (n_int < 256 ? n_int : 256);
   return sizeof(double) * (size_t)lds_doubles(v, lz_for(v, n_int, kc)) <= kLdsLimit;
@@ -1548,14 +1719,15 @@ constexpr long kResidentWaves = 2048;
 const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
   const int n_int = n_nodes - 2;
   if (n_int < 3) return nullptr;
-  if (const char* f = getenv("FDCN_VARIANT")) {  // "W,NPT" or "W,NPT,L" (L=1: single-trade)
-    int w = 0, npt = 0, lat = 0;
-    if (sscanf(f, "%d,%d,%d", &w, &npt, &lat) >= 2)
+  if (const char* f = getenv("FDCN_VARIANT")) {
+    // "W,NPT" or "W,NPT,F": F=1 single-trade flavour, F=2 paired flavour
+    int w = 0, npt = 0, fl = 0;
+    if (sscanf(f, "%d,%d,%d", &w, &npt, &fl) >= 2)
       for (int zg = 0; zg < 2; ++zg)
         for (int i = 0; i < kNumVariants; ++i)
           if (kVariants[i].it == it && kVariants[i].w == w && kVariants[i].npt == npt &&
-              kVariants[i].zg == zg && kVariants[i].lat == lat &&
-              fits(kVariants[i], n_int, k_cap, zg == 0))
+              kVariants[i].zg == zg && kVariants[i].lat == (fl == 1) &&
+              kVariants[i].pair == (fl == 2) && fits(kVariants[i], n_int, k_cap, zg == 0))
             return &kVariants[i];
   }
   const Variant* best = nullptr;
@@ -1567,7 +1739,8 @@ const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
   for (int pass = 0; pass < 3 && !best; ++pass) {
     for (int i = 0; i < kNumVariants; ++i) {
       const Variant& v = kVariants[i];
-      if (v.it != it || v.lat || v.zg != (pass == 2) || !fits(v, n_int, k_cap, pass == 0))
+      if (v.it != it || v.lat || v.pair || v.zg != (pass == 2) ||
+          !fits(v, n_int, k_cap, pass == 0))
         continue;
       const long slots = (long)64 * v.w * v.npt;
       if (!best || v.w < best_w || (v.w == best_w && slots < best_slots)) {
@@ -1586,6 +1759,14 @@ const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
     for (int i = 0; i < kNumVariants; ++i) {
       const Variant& v = kVariants[i];
       if (v.lat && v.it == it && v.w == 1 && v.npt == best->npt && !v.zg) return &v;
+    }
+  // Throughput batches of grids that fit 32 lanes of twice the chunk length:
+  // two scenarios per wave (the paired flavour, compiled for 4-node chunks,
+  // see kVariants), as long as the halved wave count still fills the chip.
+  if (best && best->w == 1 && !best->zg && !it && B >= 2 * kResidentWaves)
+    for (int i = 0; i < kNumVariants; ++i) {
+      const Variant& v = kVariants[i];
+      if (v.pair && v.it == it && v.npt == 2 * best->npt && fits(v, n_int, k_cap)) return &v;
     }
   // Small batch of long chunks without a single-trade flavour: split 48-64-
   // node chunks to ~16 across waves (config 5, one 4096-node solve: 17.1 ->

@@ -161,3 +161,51 @@ def test_rec_form_every_step_knockout_vs_oracle(ko_lo, monkeypatch):
         solves.append(s)
     assert capi.plan(n_nodes, False, B=4)["npt"] == 64
     _compare(solves, f"rec every-step KO ko_lo={ko_lo}")
+
+
+# The paired flavour (two scenarios per wave, lanes 0-31 and 32-63), forced:
+# full and partial lane use, an odd batch (the last wave's second scenario is
+# missing), per-scenario monitoring schedules and knock-out layouts, both
+# top-node layouts, accumulated tau.
+PAIR_CASES = [(8, 32 * 8 - 1, 5), (8, 32 * 8 + 1, 6), (8, 150, 4), (8, 97, 7), (8, 42, 1)]
+
+
+@pytest.mark.parametrize("npt,n_nodes,B", PAIR_CASES,
+                         ids=[f"n{npt}_{n}_{b}" for npt, n, b in PAIR_CASES])
+def test_paired_variant_vs_oracle(npt, n_nodes, B, monkeypatch):
+    monkeypatch.setenv("FDCN_VARIANT", f"1,{npt},2")
+    plan = capi.plan(n_nodes, False, B=B)
+    assert (plan["waves"], plan["npt"], plan["scen_per_block"]) == (1, npt, 2), plan
+    rng = np.random.default_rng(5000 + npt + n_nodes + B)
+    solves = []
+    for i in range(B):
+        s = random_solve(rng, n_nodes, 60, 2, it=False, drop_top=(i % 3 == 0))
+        s.tau_accumulate = (i % 4 == 1)
+        solves.append(s)
+    _compare(solves, f"cn paired NPT={npt} n={n_nodes} B={B}")
+
+
+def test_paired_every_step_knockout_vs_oracle(monkeypatch):
+    """Knock-out schedules that differ between the two scenarios of a wave:
+    every step on one, sparse on the other, rebates on both sides."""
+    monkeypatch.setenv("FDCN_VARIANT", "1,8,2")
+    n_nodes, n_time = 256, 80
+    rng = np.random.default_rng(99)
+    solves = []
+    for i in range(6):
+        s = random_solve(rng, n_nodes, n_time, 2, it=False, ko=False)
+        s.ko_lo, s.ko_hi = (10 + 9 * i, 225 - 3 * i) if i % 2 else (-1, 175)
+        s.mon_steps = list(range(1, n_time + 1)) if i % 2 == 0 else [5, 17, 18, 60, n_time]
+        s.mon_rebates = [0.5 * (i % 3)] * len(s.mon_steps)
+        solves.append(s)
+    _compare(solves, "cn paired, mixed knock-out schedules")
+
+
+def test_large_batch_picks_paired_variant():
+    big = capi.plan(256, False, B=10000)
+    assert (big["waves"], big["npt"], big["scen_per_block"]) == (1, 8, 2), big
+    small = capi.plan(256, False, B=100)
+    assert (small["waves"], small["npt"], small["scen_per_block"]) == (1, 4, 1), small
+    # config-3 grids keep one scenario per wave (the paired flavour loses there)
+    c3 = capi.plan(1024, False, B=10000)
+    assert (c3["waves"], c3["npt"], c3["scen_per_block"]) == (1, 16, 1), c3
