@@ -613,9 +613,13 @@ fdcn_march(KArgs A) {
   // fastest up to 40 nodes per lane, two at 48-64 (tools/gpu_ab_n.sh: config
   // 2 12.31 -> 12.08 ms, config 3 6.54 -> 6.21 ms, config 5 20.65 -> 19.69 ms
   // against S = 4).  The multi-wave variants serve small batches, where one
-  // wave per SIMD needs the in-wave ILP: they keep 4.
+  // wave per SIMD needs the in-wave ILP: they keep 4.  Re-measured in round 2
+  // with the current kernel (tools/gpu_ab.sh, one box, two runs each): the
+  // IT NPT = 32 variant (config 2, two waves per SIMD) is now faster with
+  // four: S = 1 11.39 ms, S = 2 11.38, S = 4 11.20; config 3 keeps one
+  // (5.91 against 6.04 with four).
   constexpr int S = (W == 1 && !(ZG & 2))
-                        ? (NPT >= 48 ? 2 : 1)
+                        ? (NPT >= 48 ? 2 : ((IT && NPT == 32) ? 4 : 1))
                         : ((NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1));
   constexpr int M = NPT / S;
 

@@ -223,11 +223,13 @@ int fdcn_session_fetch(fdcn_session* s, int32_t n, const int32_t* slots, int32_t
 
 /* ---- launch planning / introspection ---------------------------------- */
 /* Writes the kernel geometry a launch of B scenarios uses: waves per
- * scenario, nodes per lane, scenarios per workgroup, LDS bytes per workgroup,
- * and the device workspace the _dev entry points need per scenario.  Batches
- * too small to fill the chip spread each scenario over more waves, so the
- * plan depends on B; call it with the B you launch.  Any output pointer may
- * be NULL.  Returns FDCN_EINVAL if the size is unsupported. */
+ * scenario, nodes per lane, scenarios per workgroup (2: the paired flavour,
+ * two scenarios per wavefront, used for large batches of <= 256-node grids),
+ * LDS bytes per workgroup, and the device workspace the _dev entry points
+ * need per scenario.  Batches too small to fill the chip spread each scenario
+ * over more waves, so the plan depends on B; call it with the B you launch.
+ * Any output pointer may be NULL.  Returns FDCN_EINVAL if the size is
+ * unsupported. */
 int fdcn_plan(int32_t B, int32_t n_nodes, int32_t n_time, int32_t it_mode, int32_t k_cap,
               int32_t* waves, int32_t* npt, int32_t* scen_per_block, int32_t* lds_bytes,
               int64_t* ws_bytes_per_scen);
