@@ -72,6 +72,17 @@ def test_american_config2_full_grid():
     assert len(V) == rec["V_len"]
     for i, v in rec["V_sample"].items():
         assert abs(V[int(i)] - v) <= 1e-10 * max(1.0, abs(v))
+    # every node, against the oracle's march of the same plan (the golden
+    # record holds the reference's vector at every 64th node only)
+    q = AmericanFDMPricer(spot=176.39, strike=170.0, valuation_date=dt.date(2025, 7, 28),
+                          maturity_date=dt.date(2025, 8, 28), sigma=0.296783211249,
+                          option_type="put", discount_curve=c, forward_curve=c,
+                          num_space_nodes=2048, num_time_steps=4096, rannacher_steps=2,
+                          engine=oracle_engine())
+    Vo = np.asarray(q._solve_grid())
+    err = np.max(np.abs(np.asarray(V) - Vo)) / max(1.0, float(np.max(np.abs(Vo))))
+    print(f"[config2] full-vector max rel err vs oracle {err:.2e}")
+    assert err <= 1e-10
     print(f"[config2] price {p.price_log()!r} ref {rec['price_log']!r}")
     assert close("price", p.price_log(), rec["price_log"])
 

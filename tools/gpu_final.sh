@@ -1,0 +1,22 @@
+#!/bin/bash
+# End-of-round measurement session on one GPU box: the -m gpu suite, every
+# bench workload's JSON line, rocprofv3 kernel-trace summaries of the default
+# bench, and the PMC passes bench.py reads (profiles/pmc_counters.json).
+# Usage: bash tools/gpu_final.sh TAG
+set -o pipefail
+TAG=${1:-final}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 \
+    --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py > $O/bench_american.json 2> $O/bench_american.err || exit $?
+for wl in barrier double analytic scenario_file trade_cnlog trade_american trade_double; do
+  timeout -k 10 300 python bench.py --workload $wl > $O/bench_$wl.json 2> $O/bench_$wl.err || exit $?
+done
+for wl in american barrier double; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o $wl -- \
+      python3 bench.py --workload $wl --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_$wl.log 2>&1 || exit $?
+done
+bash tools/pmc_counters.sh ${TAG}_pmc american barrier double || exit $?
