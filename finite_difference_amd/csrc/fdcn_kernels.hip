@@ -357,6 +357,16 @@ struct KoLoad {  // also the paired flavour: two scenarios' masks would crowd th
 __host__ __device__ constexpr bool split_form(int it, int w, int npt) {
   return !it && (w == 16 ? npt <= 16 : npt <= 40);
 }
+// Split-form variants that tabulate their theta-form rhs terms in the
+// prologue (the one-wave throughput variants).  The latency variants (several
+// waves per scenario, or the single-trade flavour) march one scenario alone,
+// where the step's critical path is what counts: a knock-out on every step
+// (config 5) would put a table reload on every step, so they keep the raw
+// Dirichlet values and form the terms in the step (single trade, config 5:
+// 12.0 ms this way, 13.25 ms with the table).
+__host__ __device__ constexpr bool tab_form(int it, int w, int npt, int lat) {
+  return split_form(it, w, npt) && w == 1 && !lat;
+}
 
 // CN variants marched in the recovery form (W = 1, NPT > 40; see the step
 // forms in fdcn_march).  Their Rannacher steps keep the old V in a
@@ -516,7 +526,7 @@ fdcn_march(KArgs A) {
   // previous step's value and the whole term is tabulated here.
   double2* bnd = reinterpret_cast<double2*>(A.bnd) +
                  ((size_t)scen * W + wave) *
-                     (A.n_pad + kKoRow + (split_form(IT, W, NPT) ? A.n_pad : 0));
+                     (A.n_pad + kKoRow + (tab_form(IT, W, NPT, (ZG >> 1) & 1) ? A.n_pad : 0));
   const int lof = Ui(I[FDCN_I_LO_FORM]), hif = Ui(I[FDCN_I_HI_FORM]);
   const double l0 = U(P[FDCN_P_LO_C0]), l1 = U(P[FDCN_P_LO_E0]), l2 = U(P[FDCN_P_LO_C1]),
                l3 = U(P[FDCN_P_LO_E1]);
@@ -553,7 +563,7 @@ fdcn_march(KArgs A) {
   // lo_prev / hi_prev to the rebate instead: the step after one recomputes
   // its term from the raw values, kept in a second table (bnd_raw; evaluating
   // them again in the loop would keep exp's registers live in the march).
-  constexpr bool kTabSplit = split_form(IT, W, NPT);
+  constexpr bool kTabSplit = tab_form(IT, W, NPT, (ZG >> 1) & 1);
   double2* bnd_raw = bnd + A.n_pad + kKoRow;  // kTabSplit only
   (void)bnd_raw;
   {
@@ -651,7 +661,7 @@ fdcn_march(KArgs A) {
   //   CN, stencil   state V, 3-point rhs in place (shifted layout); the
   //                 multi-wave variants whose V + T would not fit the
   //                 register budget
-  constexpr bool kSplit = kTabSplit;
+  constexpr bool kSplit = split_form(IT, W, NPT);
   // CN, recover (W = 1, NPT > 40): state V only, pointwise rhs V solved in
   // place; the update x = s u - c2 V needs the old V, which the last
   // backward pass recovers from the forward-pass values it is about to
@@ -1231,7 +1241,10 @@ fdcn_march(KArgs A) {
       // itself except at the two end nodes (vb0 / vb1); the solve reads V and
       // writes T, and x = (r u)/(theta r) - c2 V afterwards.
       double blo = lo_new, bhi = hi_new;
-      if (ko_prev) {  // after a knock-out step: terms from the rebate (uniform branch)
+      if constexpr (!kTabSplit) {  // raw values: the terms of this step
+        blo = ph.th * (ph.pl * fma(ph.c2, V0, lo_new));
+        bhi = ph.th * (ph.pu * fma(ph.c2, VN, hi_new));
+      } else if (ko_prev) {  // after a knock-out step: terms from the rebate (uniform branch)
         const int kb = kPair ? ((ko_prev >> (2 * half)) & 3) : ko_prev;
         const double2 raw = bnd_raw[m];  // the step's raw Dirichlet values
         const double rlo = U(raw.x), rhi = U(raw.y);
@@ -1472,7 +1485,7 @@ fdcn_march(KArgs A) {
         }
       }
     }
-    if constexpr (!IT && !kSplit) {  // IT and kSplit read tabulated terms instead
+    if constexpr (!IT && !kTabSplit) {  // IT and kTabSplit read tabulated terms instead
       V0 = lo_new;
       VN = hi_new;
     }
@@ -1565,7 +1578,7 @@ fdcn_march(KArgs A) {
       const bool hit_me = kPair ? (half ? hit2 : hit1) : true;
       if (hit_me && 0 <= ko_lo) V0 = reb;
       if (hit_me && n_nodes - 1 >= ko_hi) VN = reb;
-      if constexpr (kSplit) {
+      if constexpr (kTabSplit) {
         // which boundary nodes the knock-out removed, per scenario (uniform)
         auto kbits = [&](int klo, int khi) { return (0 <= klo ? 1 : 0) | (n_nodes - 1 >= khi ? 2 : 0); };
         if constexpr (kPair)
@@ -1596,7 +1609,7 @@ fdcn_march(KArgs A) {
       VN = bnd_eval(hif, h0, h1, h2, h3, tau_end);
     }
   }
-  if constexpr (kSplit) {  // likewise, unless the last step knocked the node out
+  if constexpr (kTabSplit) {  // likewise, unless the last step knocked the node out
     // (the last step's raw values from the table: the loop keeps no Dirichlet
     // coefficients live)
     if (A.n_time > 0) {
@@ -1801,7 +1814,7 @@ int pad64(int n) { return ((n > 0 ? n : 1) + 63) / 64 * 64; }
 // ZG variants add the correction table [2][lz][NPT+1], rec_form variants
 // the Rannacher save slice [64][NPT]
 size_t bnd_bytes_per_scen(const Variant& v, int n_time) {
-  const size_t row = (size_t)pad64(n_time) * (split_form(v.it, v.w, v.npt) ? 2 : 1) + kKoRow;
+  const size_t row = (size_t)pad64(n_time) * (tab_form(v.it, v.w, v.npt, v.lat) ? 2 : 1) + kKoRow;
   return sizeof(double) * 2 * row * (size_t)v.w;
 }
 size_t zg_bytes_per_scen(const Variant& v, int lz) {
