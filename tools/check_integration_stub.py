@@ -33,7 +33,7 @@ class _OracleAsFdcn:
         self.fdcn_cn_batch = self._wrap(self._o.oracle_cn_batch)
         self.fdcn_it_batch = self._wrap(self._o.oracle_it_batch)
         self.fdcn_last_error = lambda: b"oracle"
-        self.fdcn_abi_version = lambda: 3
+        self.fdcn_abi_version = lambda: 4
 
     @staticmethod
     def _wrap(fn):
