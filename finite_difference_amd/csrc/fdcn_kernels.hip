@@ -438,6 +438,10 @@ struct KArgs {
 // nodes -- twice the nodes per lane of the one-scenario variant for the same
 // grid, so the per-step scans, carries and broadcasts are spread over twice
 // as many nodes.  Its per-scenario constants are per-lane values (VGPRs).
+// LDS doubles for the scan weights of stages 2-5 (forward and backward, 64
+// lanes): Geo::kScanLds variants
+constexpr int kScanLdsDoubles = 4 * 2 * 64;
+
 template <int IT, int W, int NPT, int ZG = 0>
 struct Geo {
   static constexpr bool kPair = (ZG & 4) != 0;
@@ -446,13 +450,16 @@ struct Geo {
   // IT payoff staged in LDS unless it would not fit (8+ waves per scenario)
   static constexpr bool kPhiLds = IT && (W <= 4);
   static constexpr int kThreads = kPair ? 64 : 64 * W * SPB;
+  // one-wave CN variants keep the weights of scan stages 2-5 in LDS (see
+  // setup_scan); IT's LDS already holds the payoff
+  static constexpr bool kScanLds = !IT && W == 1;
 };
 
 // doubles of LDS per scenario
 template <int IT, int W, int NPT, int ZG = 0>
 __host__ __device__ inline int lds_doubles_per_scen(int lz) {
   return ((ZG & 1) ? 0 : 2 * lz * (NPT + 1)) + (Geo<IT, W, NPT, ZG>::kPhiLds ? 64 * W * NPT : 0) +
-         (W > 1 ? Xch<W>::kSize : 0);
+         (W > 1 ? Xch<W>::kSize : 0) + (Geo<IT, W, NPT, ZG>::kScanLds ? kScanLdsDoubles : 0);
 }
 
 // Issue priority of the zero-carry passes and the carry scans.  Each sweep
@@ -466,8 +473,16 @@ __host__ __device__ inline int lds_doubles_per_scen(int lz) {
 // 3 neutral; raising it over the Sherman-Morrison broadcast lost time.
 #define FDCN_PRIO_HI() __builtin_amdgcn_s_setprio(3)
 #define FDCN_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+// Occupancy target: the config-3 throughput variant (CN, one wave, 16-node
+// chunks) is held to 128 VGPRs, 4 waves per SIMD instead of 3 (measured
+// 5.56 -> 5.44 ms per launch with the scan weights of stages 2-5 in LDS,
+// against 5.94 before both); every other variant is unconstrained (1).
+template <int IT, int W, int NPT, int ZG>
+constexpr int kWavesPerEu = (!IT && W == 1 && NPT == 16 && !(ZG & 6)) ? 4 : 1;
+
 template <int IT, int W, int NPT, int ZG = 0>
 __global__ void __launch_bounds__(64 * W)
+__attribute__((amdgpu_waves_per_eu(kWavesPerEu<IT, W, NPT, ZG>)))
 fdcn_march(KArgs A) {
   constexpr int L = Geo<IT, W, NPT, ZG>::L;
   constexpr int SPB = Geo<IT, W, NPT, ZG>::SPB;
@@ -504,6 +519,12 @@ fdcn_march(KArgs A) {
   double* ztab = (ZG & 1) ? A.zg + (size_t)scen * 2 * lz * (NPT + 1) : my;
   double* phit = my + ((ZG & 1) ? 0 : 2 * lz * (NPT + 1));  // payoff [NPT][L] (kPhiLds)
   double* xch = phit + (kPhiLds ? L * NPT : 0);       // exchange area (W > 1)
+  constexpr bool kScanLds = Geo<IT, W, NPT, ZG>::kScanLds;
+  // scan weights of stages 2-5 (kScanLds), [stage-2][fwd, bwd][lane]; a paired
+  // wave's two scenarios share the wave's one set (weights are per lane)
+  double* sw = (kPair ? lds : xch + (W > 1 ? Xch<W>::kSize : 0)) +
+               (kPair ? 2 * lds_doubles_per_scen<IT, W, NPT, ZG>(lz) - kScanLdsDoubles : 0);
+  (void)sw;
   (void)xch;
 
   const double* P = A.params + (size_t)scen * FDCN_NPARAM;
@@ -723,6 +744,15 @@ fdcn_march(KArgs A) {
     }
     Fpre = f;
     Gsuf = g;
+    if constexpr (kScanLds) {
+      // stages 2-5 are rare (only when |fm|^(NPT-1) > 3e-5): their weights
+      // wait in LDS, so only stages 0-1 hold registers in the march
+#pragma unroll
+      for (int j = 2; j < 6; ++j) {
+        sw[(j - 2) * 128 + lane] = FW[j];
+        sw[(j - 2) * 128 + 64 + lane] = GW[j];
+      }
+    }
     // After j Hillis-Steele stages lane t holds the contributions of lanes
     // t-2^j+1..t; the rest is scaled by at most q^(2^j), q = |fm|^(NPT-1)
     // (a short lane's product, the largest).  Stop once that is <= 1e-18:
@@ -790,7 +820,21 @@ fdcn_march(KArgs A) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      if (j < nst_f) b = fma(FW[j], scan_up(b, d, lane4), b);
+      if constexpr (W == 1) {
+        // stages 0-1 unconditionally (a stage below the 1e-18 cut only adds
+        // a negligible term), the rest behind one uniform branch
+        if (j < 2) b = fma(FW[j], scan_up(b, d, lane4), b);
+      } else if (j < nst_f) {
+        b = fma(FW[j], scan_up(b, d, lane4), b);
+      }
+    }
+    if (W == 1 && nst_f > 2) {
+#pragma unroll
+      for (int j = 2; j < 6; ++j) {
+        const int d = 1 << j;
+        const double wf = kScanLds ? sw[(j - 2) * 128 + lane] : FW[j];
+        if (j < nst_f) b = fma(wf, scan_up(b, d, lane4), b);
+      }
     }
     double cw = 0.0;
     if constexpr (W > 1) {
@@ -844,7 +888,19 @@ fdcn_march(KArgs A) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      if (j < nst_b) cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
+      if constexpr (W == 1) {
+        if (j < 2) cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
+      } else if (j < nst_b) {
+        cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
+      }
+    }
+    if (W == 1 && nst_b > 2) {
+#pragma unroll
+      for (int j = 2; j < 6; ++j) {
+        const int d = 1 << j;
+        const double wg = kScanLds ? sw[(j - 2) * 128 + 64 + lane] : GW[j];
+        if (j < nst_b) cb = fma(wg, scan_dn(cb, d, lane4), cb);
+      }
     }
     double cwb = 0.0;
     if constexpr (W > 1) {
