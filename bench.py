@@ -33,6 +33,9 @@ out -- VERDICT r1 item 7):
   scenario_file   configs[2] numerics: 10 000 rows (KO / KI / vanilla, one
                   option type per file), explicit 1024 x 2000, priced by
                   scenario_batch.price_columns + result_columns
+  american_file   configs[1] numerics: 2 000 American put rows (strike / vol /
+                  spot sweep, two curves), 2048 x 4096, price_log2 +
+                  greeks_log2 of every row by american_batch.price_columns
 
 value = total node-steps (configured nodes x steps x B x ranks) / max-over-
 ranks wall time of the K timed launches (whole-job aggregate).
@@ -75,7 +78,8 @@ N_SIMD = 1024
 BYTES_PER_NODE_STEP = {True: 32, False: 16}   # IT: V and lambda in+out; CN: V in+out
 FLOPS_PER_NODE_STEP = {True: 17, False: 10}
 DEFAULT_BATCH = {"american": 4096, "barrier": 10000, "double": 2048, "analytic": 1 << 20}
-TRADE_WORKLOADS = ("trade_cnlog", "trade_american", "trade_double", "scenario_file")
+TRADE_WORKLOADS = ("trade_cnlog", "trade_american", "trade_double", "scenario_file",
+                   "american_file")
 KERNEL_SRC = os.path.join(ROOT, "finite_difference_amd", "csrc", "fdcn_kernels.hip")
 
 
@@ -326,6 +330,8 @@ def run_rank(args):
         return bench_analytic(args)
     if args.workload == "scenario_file":
         return bench_scenario_file(args)
+    if args.workload == "american_file":
+        return bench_american_file(args)
     if args.workload in TRADE_WORKLOADS:
         return bench_trade(args)
     import numpy as np
@@ -570,6 +576,58 @@ def bench_scenario_file(args):
                    "rows": R, "pde_rows": n_pde, "solves": 2 * n_pde},
         "host_ms": ms - march_ms, "plan_ms": sum(plans) / len(plans) * 1e3,
         "march_and_epilogue_ms": march_ms,
+        "outputs_finite": bool(np.all(np.isfinite(out["model_price"])))}), flush=True)
+
+
+def bench_american_file(args):
+    """A 2 000-row American scenario file priced end to end per step
+    (price_log2 + greeks_log2 of every row: six unique grids each)."""
+    import numpy as np
+    from finite_difference_amd import american_batch, capi, distributed
+    from finite_difference_amd.engine import Engine
+    if distributed.bind_device() is None:
+        raise capi.FdcnError("no gfx950 device visible; the benchmark needs an MI355X")
+    R = args.batch or 2000
+    N, M = args.n_space or 2048, args.n_time or 4096
+    rng = np.random.default_rng(20250728)
+    cols = {"scenario_name": [f"a{i}" for i in range(R)],
+            "S0": (176.39 * rng.uniform(0.9, 1.1, R)).tolist(),
+            "K": rng.uniform(150, 200, R).tolist(), "sigma": rng.uniform(0.2, 0.4, R).tolist(),
+            "rate": [(0.0705, 0.065)[i % 2] for i in range(R)],
+            "FA_price": [5.0] * R, "FA_delta": [-0.4] * R, "FA_gamma": [0.02] * R,
+            "FA_vega": [0.2] * R}
+    base = dict(valuation=dt.date(2025, 7, 28), maturity=dt.date(2025, 8, 28), opt_type="put",
+                num_space_nodes=N, num_time_steps=M)
+    eng = Engine()
+
+    def one(timing):
+        res = american_batch.price_columns(cols, base, eng, timing=timing)
+        return american_batch.result_columns(cols, res)
+    for _ in range(args.warmup):
+        one({})
+    walls, plans, marches = [], [], []
+    out = None
+    for _ in range(args.steps):
+        tm = {}
+        t0 = time.perf_counter()
+        out = one(tm)
+        walls.append(time.perf_counter() - t0)
+        plans.append(tm["plan"])
+        marches.append(tm["march"])
+    ms = sum(walls) / len(walls) * 1e3
+    march_ms = sum(marches) / len(marches) * 1e3
+    node_steps = R * (5 * N * M + N * 2 * M)  # N, sigma +-h, +-2h at M steps; 2M
+    print(json.dumps({
+        "metric": "American scenario file wall time (run_all_american_scenarios pricing)",
+        "value": ms, "unit": "ms/file", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "ms_min": min(walls) * 1e3,
+        "higher_is_better": False, "scaling": "none", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic American put file (notebook trade swept over spot, strike, vol; "
+                "two curves)",
+        "config": {"workload": f"american_file_{R}rows_{N}x{M}", "config": "BASELINE configs[1]",
+                   "rows": R, "grids_per_row": 6},
+        "host_ms": ms - march_ms, "plan_ms": sum(plans) / len(plans) * 1e3,
+        "march_and_epilogue_ms": march_ms, "node_steps_per_s": node_steps / (ms * 1e-3),
         "outputs_finite": bool(np.all(np.isfinite(out["model_price"])))}), flush=True)
 
 

@@ -41,7 +41,7 @@ EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batc
             "fdcn_session_destroy", "fdcn_session_slots", "fdcn_session_march",
             "fdcn_session_dividend_jump", "fdcn_session_greeks", "fdcn_session_fetch",
             "fdcn_vc_batch", "fdcn_vc_batch_dev", "fdcn_vc_plan", "fdcn_barrier_plan",
-            "fdcn_vmath")
+            "fdcn_vmath", "fdcn_american_plan")
 VC_NDIAG = 6
 RR_NPARAM, RR_NFLAG = 8, 5
 DB_NPARAM, DB_NFLAG = 8, 3
@@ -139,6 +139,9 @@ def lib() -> ctypes.CDLL:
             L.fdcn_barrier_plan.argtypes = [_I, _V, _V, ctypes.c_double, _I, _I, _I, _I,
                                             ctypes.c_double, ctypes.c_double, _I, _I, _V, _V,
                                             _V, _V, _V, _V, _V, _V, _V]
+            L.fdcn_american_plan.restype = _I
+            L.fdcn_american_plan.argtypes = [_I, _V, _V, _I, ctypes.c_double, ctypes.c_double,
+                                             _V, _V, _V, _V, _V, _V, _V]
             L.fdcn_vmath.restype = _I
             L.fdcn_vmath.argtypes = [_I, ctypes.c_int64, _V, _V]
             L.fdcn_select_device.restype = ctypes.c_int
@@ -299,6 +302,29 @@ def vmath(op: int, x) -> np.ndarray:
 
 
 BP_NROW, BP_NFLAG = 10, 4  # FDCN_BP_NROW / FDCN_BP_NFLAG
+AP_NJOB, AP_NOUT = 5, 4    # FDCN_AP_NJOB / FDCN_AP_NOUT
+
+
+def american_plan(job: np.ndarray, call: np.ndarray, n_space: int, s_max_mult: float,
+                  T: float, with_grids: bool = False) -> dict:
+    """fdcn_american_plan: grid, payoff, coefficients and readouts of J
+    American (row, sigma) jobs, host only (see include/fdcn.h)."""
+    job = np.ascontiguousarray(job, np.float64)
+    call = np.ascontiguousarray(call, np.int32)
+    J = job.shape[0]
+    if job.shape != (J, AP_NJOB) or call.shape != (J,):
+        raise ValueError("american_plan: job [J, 5] and call [J] expected")
+    n1 = int(n_space) + 1
+    out = dict(params=np.empty((J, NPARAM)), iparams=np.empty((J, NIPARAM), np.int32),
+               payoff=np.empty((J, n1)), s_nodes=np.empty((J, n1)) if with_grids else None,
+               rint=np.empty((2 * J, GK_NRINT), np.int32), rdbl=np.empty((2 * J, GK_NRDBL)),
+               gout=np.empty((J, AP_NOUT)))
+    _check(lib().fdcn_american_plan(
+        J, job.ctypes.data, call.ctypes.data, int(n_space), float(s_max_mult), float(T),
+        out["params"].ctypes.data, out["iparams"].ctypes.data, out["payoff"].ctypes.data,
+        out["s_nodes"].ctypes.data if with_grids else None, out["rint"].ctypes.data,
+        out["rdbl"].ctypes.data, out["gout"].ctypes.data))
+    return out
 GK_NPARAM, GK_NRINT, GK_NRDBL = 8, 5, 8
 
 

@@ -273,4 +273,121 @@ int fdcn_barrier_plan(int32_t R, const double* row, const int32_t* rflag, double
   return FDCN_OK;
 }
 
+int fdcn_american_plan(int32_t J, const double* job, const int32_t* call, int32_t n_space,
+                       double s_max_mult, double T, double* params, int32_t* iparams,
+                       double* payoff, double* s_nodes, int32_t* rint, double* rdbl,
+                       double* gout) {
+#pragma clang fp contract(off)
+  if (J < 0 || n_space < 3)
+    return pfail(FDCN_EINVAL, "fdcn_american_plan: J >= 0, n_space >= 3");
+  if (J == 0) return FDCN_OK;
+  if (!job || !call || !params || !iparams || !payoff || !rint || !rdbl || !gout)
+    return pfail(FDCN_EINVAL, "fdcn_american_plan: NULL argument");
+  const int32_t n = n_space;  // nodes 0..n
+  parallel_for(J, 8, [&](int64_t q) {
+    const double* jb = job + q * FDCN_AP_NJOB;
+    const double spot = jb[FDCN_AP_SPOT], K = jb[FDCN_AP_STRIKE], sig = jb[FDCN_AP_SIGMA];
+    const double b = jb[FDCN_AP_CARRY], r = jb[FDCN_AP_DISC];
+    const bool is_call = call[q] != 0;
+    // _configure_grid (fd_american_equity.py:340-361), Python min/max order
+    const double s_low = (K < spot) ? K : spot;    // min(spot, strike)
+    const double s_high = (K > spot) ? K : spot;   // max(spot, strike)
+    const double prod = s_low * s_high;
+    const double s_c = ::sqrt(1e-12 > prod ? 1e-12 : prod);
+    const double band = s_max_mult * sig * ::sqrt(1e-12 > T ? 1e-12 : T);
+    const double x_c = ::log(s_c);
+    double s_min = ::exp(x_c - 0.5 * band), s_max = ::exp(x_c + 0.5 * band);
+    if (0.5 * s_low < s_min) s_min = 0.5 * s_low;
+    if (2.0 * s_high > s_max) s_max = 2.0 * s_high;
+    if (1e-8 > s_min) s_min = 1e-8;
+    // _build_log_grid (:363-384)
+    const double x_min = ::log(s_min), x_max = ::log(s_max);
+    const double dx = (x_max - x_min) / (double)n;
+    std::vector<double> sv((size_t)n + 1);
+    double* s = s_nodes ? s_nodes + q * (int64_t)(n + 1) : sv.data();
+    for (int32_t i = 0; i <= n; ++i) s[i] = ::exp(x_min + (double)i * dx);
+    // _snap_critical_levels_to_grid (:386-407): argmin |s - x|, first on ties
+    auto nearest = [&](double x) -> int32_t {
+      const int64_t j = lower(s, 0, (int64_t)n + 1, x);
+      if (j <= 0) return 0;
+      if (j > n) return n;
+      return (::fabs(s[j - 1] - x) <= ::fabs(s[j] - x)) ? (int32_t)(j - 1) : (int32_t)j;
+    };
+    const int32_t is = nearest(spot), ik = nearest(K);
+    const double s0 = s[is], ks = s[ik];
+    // payoff with the snapped strike (Python max(e, 0.0))
+    double* pf = payoff + q * (int64_t)(n + 1);
+    for (int32_t i = 0; i <= n; ++i) {
+      const double e = is_call ? s[i] - ks : ks - s[i];
+      pf[i] = (0.0 > e) ? 0.0 : e;
+    }
+    // operator coefficients (q = 0: discrete dividends are jumps)
+    const double sig2 = sig * sig;
+    const double mu_x = (b - 0.0) - 0.5 * sig2;
+    const double alpha = 0.5 * sig2 / (dx * dx);
+    const double beta_adv = mu_x / (2.0 * dx);
+    double* P = params + q * FDCN_NPARAM;
+    for (int k = 0; k < FDCN_NPARAM; ++k) P[k] = 0.0;
+    P[FDCN_P_A] = alpha - beta_adv;
+    P[FDCN_P_C] = alpha + beta_adv;
+    P[FDCN_P_BC] = -2.0 * alpha - r;
+    // Dirichlet values (:430-448): call top s_N e^{(b-r)tau} - K e^{-r tau};
+    // put bottom K e^{-r tau}
+    if (is_call) {
+      P[FDCN_P_HI_C0] = s[n];
+      P[FDCN_P_HI_E0] = b - r;
+      P[FDCN_P_HI_C1] = -ks;
+      P[FDCN_P_HI_E1] = -r;
+    } else {
+      P[FDCN_P_LO_C0] = ks;
+      P[FDCN_P_LO_E0] = -r;
+    }
+    int32_t* I = iparams + q * FDCN_NIPARAM;
+    for (int k = 0; k < FDCN_NIPARAM; ++k) I[k] = 0;
+    I[FDCN_I_KO_LO] = -1;
+    I[FDCN_I_KO_HI] = n + 2;  // none (>= n_nodes, as engine.pack clamps it)
+    I[FDCN_I_TAU_MODE] = 1;   // tau = tau + dt (fd_american_equity.py:664-724)
+    // readouts at the snapped spot (_interp_price :855-874): interpolation
+    // only (row 2q), and with the cubic Delta/Gamma (:876-907) around the
+    // nearest node clamped to [1, n-2] (row 2q+1); slot field = job index
+    for (int c = 0; c < 2; ++c) {
+      int32_t* ri = rint + (2 * q + c) * FDCN_GK_NRINT;
+      double* rd = rdbl + (2 * q + c) * FDCN_GK_NRDBL;
+      for (int k = 0; k < FDCN_GK_NRDBL; ++k) rd[k] = 0.0;
+      ri[0] = (int32_t)q;
+      if (s0 <= s[0]) {
+        ri[1] = 1;
+        ri[2] = 0;
+      } else if (s0 >= s[n]) {
+        ri[1] = 2;
+        ri[2] = n;
+      } else {
+        const int64_t hi = upper(s, 0, (int64_t)n + 1, s0);
+        ri[1] = 0;
+        ri[2] = (int32_t)(hi - 1);
+        rd[1] = s[hi - 1];
+        rd[2] = s[hi];
+      }
+      rd[0] = s0;
+      if (c == 0) {
+        ri[3] = 0;
+        ri[4] = 0;
+      } else {
+        int32_t i = is;  // argmin |s - s0| = the snapped index
+        i = i < 1 ? 1 : (i > n - 2 ? n - 2 : i);
+        ri[3] = i;
+        ri[4] = 2;
+        rd[3] = s0;
+        for (int k = 0; k < 4; ++k) rd[4 + k] = s[i - 1 + k];
+      }
+    }
+    double* g = gout + q * FDCN_AP_NOUT;
+    g[0] = s0;
+    g[1] = ks;
+    g[2] = dx;
+    g[3] = (double)is;
+  });
+  return FDCN_OK;
+}
+
 }  // extern "C"

@@ -307,17 +307,22 @@ def run_all_american_scenarios(config_csv_path: str, output_csv_path: Optional[s
     """run_american_scenarios.py:209-277 with every grid of the file batched."""
     import pandas as pd
     from . import distributed
+    from . import american_batch
     cfg = pd.read_csv(config_csv_path)
     if distributed.is_initialized():
         distributed.bind_device()
     rows = distributed.shard([dict(r) for _, r in cfg.iterrows()])
-    pricers = [make_american_pricer(r["S0"], r["K"], r["sigma"], r["rate"], engine=engine,
-                                    **base_params) for r in rows]
-    prefetch_many(pricers)
-    res = [_result_row(r["scenario_name"], r["S0"], r["K"], r["sigma"], r["rate"], {},
-                       p.price_log2(), p.greeks_log2(), _opt(r, "FA_price"),
-                       _opt(r, "FA_delta"), _opt(r, "FA_gamma"), _opt(r, "FA_vega"))
-           for r, p in zip(rows, pricers)]
+    # the whole shard in one plan build, lock-step launches and one epilogue
+    # (american_batch.py); the per-row façades when it declines
+    res = american_batch.run_rows_vectorized(rows, base_params, engine)
+    if res is None:
+        pricers = [make_american_pricer(r["S0"], r["K"], r["sigma"], r["rate"], engine=engine,
+                                        **base_params) for r in rows]
+        prefetch_many(pricers)
+        res = [_result_row(r["scenario_name"], r["S0"], r["K"], r["sigma"], r["rate"], {},
+                           p.price_log2(), p.greeks_log2(), _opt(r, "FA_price"),
+                           _opt(r, "FA_delta"), _opt(r, "FA_gamma"), _opt(r, "FA_vega"))
+               for r, p in zip(rows, pricers)]
     res = distributed.gather_rows(res)
     if res is None:
         return None

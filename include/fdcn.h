@@ -368,6 +368,25 @@ int fdcn_barrier_plan(int32_t R, const double* row, const int32_t* rflag, double
                       const int32_t* mon_k, double* params, int32_t* iparams, double* v_init,
                       double* mon_rebate, int32_t* rint, double* rdbl, double* tparams,
                       int32_t* n_nodes_out);
+/* American counterpart (run_american_scenarios.py:209-277 over
+ * AmericanFDMPricer, fd_american_equity.py:340-448, :855-907): the log grid
+ * of one (row, sigma) job each -- band around sqrt(S K), uniform log nodes,
+ * spot and strike snapped to the nearest node, payoff with the snapped
+ * strike, operator coefficients (q = 0), Dirichlet forms, TAU_MODE 1 -- and
+ * its two readouts at the snapped spot.  n_space + 1 nodes per job.
+ *   job [J][FDCN_AP_NJOB] = spot, strike, sigma, carry, r;  call [J] (1 call, 0 put)
+ *   params [J][FDCN_NPARAM]: DT and TAU0 left 0 (set per segment by the caller)
+ *   iparams [J][FDCN_NIPARAM], payoff [J][n_space+1], s_nodes [J][n_space+1]
+ *   (may be NULL), rint / rdbl [2J]: row 2q the interpolation readout, row
+ *   2q+1 with the cubic Delta/Gamma (fdcn_session_greeks layout, slot = q),
+ *   gout [J][FDCN_AP_NOUT] = snapped spot, snapped strike, dx, spot index. */
+#define FDCN_AP_NJOB 5
+enum fdcn_ap_job { FDCN_AP_SPOT = 0, FDCN_AP_STRIKE, FDCN_AP_SIGMA, FDCN_AP_CARRY, FDCN_AP_DISC };
+#define FDCN_AP_NOUT 4
+int fdcn_american_plan(int32_t J, const double* job, const int32_t* call, int32_t n_space,
+                       double s_max_mult, double T, double* params, int32_t* iparams,
+                       double* payoff, double* s_nodes, int32_t* rint, double* rdbl,
+                       double* gout);
 /* y = exp(x) (op 0), log(x) (1), sqrt(x) (2), pow(x, 2.0) (3) elementwise with
  * the C library (the functions CPython's math module and float ** call). */
 int fdcn_vmath(int32_t op, int64_t n, const double* x, double* y);

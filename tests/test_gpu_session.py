@@ -240,3 +240,27 @@ def test_run_all_scenarios_file_on_device(tmp_path):
     for i, r in enumerate(ref):
         for k in ("model_price", "model_delta", "model_gamma", "model_vega"):
             assert abs(df[k].iloc[i] - r[k]) <= 1e-9 * max(1.0, abs(r[k])), (i, k)
+
+
+@pytest.mark.parametrize("divs", [None, [(__import__("datetime").date(2025, 8, 11), 1.5)]],
+                         ids=["nodiv", "div1"])
+def test_vectorized_american_file_equals_per_row_device(divs):
+    """american_batch (native plan, lock-step segment launches, device jumps
+    and epilogue) against the per-row façades' device path (greeks_many) on
+    the same GPU: the same grids in launches of the same shapes, so bitwise."""
+    import test_american_batch as T
+    from finite_difference_amd import american_batch
+    from finite_difference_amd.american import prefetch_many
+    for opt in ("put", "call"):
+        base = T._base(opt, divs, n=128, m=96)
+        rows = T._rows(12, 4)
+        ps = [scenarios.make_american_pricer(r["S0"], r["K"], r["sigma"], r["rate"],
+                                             engine=Engine(), **base) for r in rows]
+        prefetch_many(ps)
+        cols = {k: [r[k] for r in rows] for k in american_batch.ROW_KEYS}
+        res = american_batch.price_columns(cols, base, Engine())
+        for i, p in enumerate(ps):
+            assert res["price_log2"][i] == p.price_log2(), (opt, i)
+            g = p.greeks_log2()
+            for k in ("price", "delta", "gamma", "vega", "theta"):
+                assert res[k][i] == g[k], (opt, i, k, res[k][i], g[k])
