@@ -163,13 +163,16 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
     t1 = time.perf_counter()
 
     def group(members: np.ndarray, nt: int, seg: int, v_init) -> Group:
+        # v_init None: the first segment, which starts from the payoff (one
+        # array for both, so a session stages it once)
         _, pts, steps = segs[nt]
         P = plan["params"][members].copy()
         P[:, capi.P_DT] = (pts[seg + 1] - pts[seg]) / float(steps[seg])
         P[:, capi.P_TAU0] = pts[seg]
         restart = seg == 0 or call
+        pay = plan["payoff"][members]
         return Group(True, n1, int(steps[seg]), p0.rannacher_steps if restart else 0, P,
-                     plan["iparams"][members], v_init, plan["payoff"][members],
+                     plan["iparams"][members], pay if v_init is None else v_init, pay,
                      np.zeros(0, np.int32), np.zeros(0), list(members))
 
     members = {nt: np.nonzero(job_nt == nt)[0] for nt in nts}
@@ -184,7 +187,8 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
                     if seg >= len(steps) or steps[seg] < 1:
                         continue
                     m = members[nt]
-                    g = group(m, nt, seg, plan["payoff"][m] if seg == 0 else None)
+                    # later segments start from the slots (no host vector)
+                    g = group(m, nt, seg, None if seg == 0 else np.empty((len(m), 0)))
                     slot[m] = S.march(g, None if seg == 0 else slot[m])
                     eng.launches += 1
                     eng.solves += len(m)
@@ -213,7 +217,7 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
                 if seg >= len(steps) or steps[seg] < 1:
                     continue
                 m = members[nt]
-                v0 = plan["payoff"][m] if seg == 0 else np.stack([V[j] for j in m])
+                v0 = None if seg == 0 else np.stack([V[j] for j in m])
                 out = eng.backend.run_group(group(m, nt, seg, v0))
                 eng.launches += 1
                 eng.solves += len(m)

@@ -171,8 +171,9 @@ int fdcn_session_slots(const fdcn_session* s);  /* slots created so far */
 
 /* One batched march (the fdcn_cn_batch / fdcn_it_batch plan; it != 0 for
  * Ikonen-Toivanen).  Initial vectors come from the host (v_init [B][n_nodes])
- * or from earlier slots (v_init_slots [B]); pass exactly one.  The B outputs
- * become new slots, numbers written to out_slots [B]. */
+ * or from earlier slots (v_init_slots [B]); pass exactly one.  An IT march
+ * may pass its payoff pointer as v_init (the array is staged once).  The B
+ * outputs become new slots, numbers written to out_slots [B]. */
 int fdcn_session_march(fdcn_session* s, int32_t it, int32_t B, int32_t n_nodes, int32_t n_time,
                        int32_t n_ranna, const double* params, const int32_t* iparams,
                        const double* v_init, const int32_t* v_init_slots, const double* payoff,
