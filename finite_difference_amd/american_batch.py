@@ -243,7 +243,7 @@ ROW_KEYS = ("scenario_name", "S0", "K", "sigma", "rate", "FA_price", "FA_delta",
 def result_columns(cols: Dict[str, Sequence], res: Dict[str, np.ndarray]) -> Dict[str, Any]:
     """run_american_scenarios.py's result schema (scenarios._result_row with
     model_price = price_log2, Greeks from greeks_log2) as columns."""
-    from .scenario_batch import _opt_col, _pct_diff
+    from .scenario_batch import _num_col, _pct_diff
     R = len(cols["S0"])
     out: Dict[str, Any] = {}
     for k in ("scenario_name", "S0", "K", "sigma", "rate"):
@@ -251,8 +251,7 @@ def result_columns(cols: Dict[str, Sequence], res: Dict[str, np.ndarray]) -> Dic
     for name, key in (("price", "price_log2"), ("delta", "delta"), ("gamma", "gamma"),
                       ("vega", "vega")):
         model = np.asarray(res[key], np.float64)
-        fa = np.array([np.nan if v is None else float(v)
-                       for v in _opt_col(cols, f"FA_{name}", R)], np.float64)
+        fa = _num_col(cols, f"FA_{name}", R)
         out[f"model_{name}"] = model
         out[f"FA_{name}"] = fa
         out[f"{name}_diff"] = np.abs(model - fa)

@@ -58,6 +58,19 @@ def _opt_col(cols: Dict[str, Sequence], key: str, R: int) -> List[Any]:
     return [None if _missing(v) else v for v in c]
 
 
+def _num_col(cols: Dict[str, Sequence], key: str, R: int) -> np.ndarray:
+    """A numeric optional column as float64 with NaN for missing cells (None
+    or NaN, as _missing); numpy's own conversion when every cell is a number
+    or None, the per-cell test otherwise."""
+    c = cols.get(key)
+    if c is None:
+        return np.full(R, np.nan)
+    try:
+        return np.asarray(c, dtype=np.float64).reshape(R)
+    except (TypeError, ValueError):
+        return np.array([np.nan if _missing(v) else float(v) for v in c], np.float64)
+
+
 def _black76(S, K, sigma, t_exp, carry, t_carry, r, t_disc, pv, call):
     """_vanilla_black76_price (:648-692) elementwise, same operation order;
     math.exp / math.log through libm (capi.vmath), math.sqrt = np.sqrt
@@ -180,25 +193,27 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
     S0 = np.asarray(cols["S0"], np.float64)
     K = np.asarray(cols["K"], np.float64)
     sig = np.asarray(cols["sigma"], np.float64)
-    rate = [float(x) for x in cols["rate"]]
-    bts = [str(b).lower() for b in cols["barrier_type"]]
-    ups = _opt_col(cols, "upper_barrier", R)
-    los = _opt_col(cols, "lower_barrier", R)
+    rate = np.asarray(cols["rate"], np.float64).reshape(R)
+    # barrier kinds through the distinct strings of the column
+    ub, binv = np.unique(np.asarray([str(b) for b in cols["barrier_type"]]), return_inverse=True)
+    bts_u = [b.lower() for b in ub.tolist()]
+    ups = _num_col(cols, "upper_barrier", R)
+    los = _num_col(cols, "lower_barrier", R)
     if np.any(~(S0 > 0)) or np.any(~(K > 0)) or np.any(~(sig > 0)):
         raise ValueError("spot, strike, sigma must be positive.")
-    for b in bts:
+    for b in bts_u:
         if b != "none" and b not in KO_KIND and b not in KI_KIND:
             raise ValueError(f"Unsupported barrier_type: {b}")
-    # per-rate scalars (one facade per rate, as run_rows_batched)
-    first: Dict[float, int] = {}
-    for i, rt in enumerate(rate):
-        first.setdefault(rt, i)
-    rates = list(first)
-    per_rate = [scenarios.make_barrier_pricer(float(S0[i]), float(K[i]), float(sig[i]), rt,
-                                              "none", None, None, **bp)
-                for rt, i in first.items()]
-    pos = {rt: j for j, rt in enumerate(rates)}
-    rix = np.fromiter((pos[x] for x in rate), np.int64, R)
+    # per-rate scalars (one facade per rate, in order of first appearance, as
+    # run_rows_batched)
+    ur, first_ix, rinv = np.unique(rate, return_index=True, return_inverse=True)
+    order = np.argsort(first_ix, kind="stable")
+    pos = np.empty(len(order), np.int64)
+    pos[order] = np.arange(len(order))
+    rix = pos[rinv.reshape(R)]
+    per_rate = [scenarios.make_barrier_pricer(float(S0[i]), float(K[i]), float(sig[i]),
+                                              float(rate[i]), "none", None, None, **bp)
+                for i in first_ix[order].tolist()]
     p0 = per_rate[0]
     T, t_carry, t_disc = p0.time_to_expiry, p0.time_to_carry, p0.time_to_discount
     carry = np.array([p.carry_rate_nacc for p in per_rate])[rix]
@@ -216,23 +231,21 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
     already_in = bool(bp.get("already_in", False))
 
     out = {k: np.zeros(R) for k in GREEKS}
-    kind = np.zeros(R, np.int32)
-    for i, b in enumerate(bts):
-        if b in KO_KIND and not already_hit:
-            kind[i] = KO_KIND[b]
-        elif b in KI_KIND and not already_in:
-            kind[i] = KI_KIND[b]
+    binv = binv.reshape(R)
+    is_ko = np.array([b in KO_KIND for b in bts_u], bool)[binv]
+    kind_u = [KO_KIND[b] if b in KO_KIND and not already_hit else
+              KI_KIND[b] if b in KI_KIND and not already_in else 0 for b in bts_u]
+    kind = np.asarray(kind_u, np.int32)[binv]
     pde = np.nonzero(kind)[0]
     if len(pde):
         Rp = len(pde)
         row = np.zeros((Rp, capi.BP_NROW))
         flag = np.zeros((Rp, capi.BP_NFLAG), np.int32)
         row[:, 0], row[:, 1], row[:, 2] = S0[pde], K[pde], sig[pde]
-        for j, i in enumerate(pde):
-            if los[i] is not None:
-                row[j, 3], flag[j, 2] = float(los[i]), 1
-            if ups[i] is not None:
-                row[j, 4], flag[j, 3] = float(ups[i]), 1
+        has_lo, has_up = ~np.isnan(los[pde]), ~np.isnan(ups[pde])
+        row[:, 3] = np.where(has_lo, los[pde], 0.0)
+        row[:, 4] = np.where(has_up, ups[pde], 0.0)
+        flag[:, 2], flag[:, 3] = has_lo, has_up
         row[:, 5], row[:, 6], row[:, 7], row[:, 8] = carry[pde], divy[pde], disc[pde], pv[pde]
         row[:, 9] = float(bp.get("rebate_amount", 0.0))
         flag[:, 0] = 0 if call else 1
@@ -260,14 +273,12 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
             out[k][pde] = res[:, j]
     # knocked-out rows (already_hit, :907-946): the rebate discounted from the
     # discount end date, zero Greeks
-    if already_hit:
-        for i, b in enumerate(bts):
-            if b in KO_KIND:
-                p = per_rate[rix[i]]
-                out["price"][i] = bp.get("rebate_amount", 0.0) * p.get_discount_factor(
-                    p.discount_end_date)
+    if already_hit and np.any(is_ko):
+        reb = np.array([bp.get("rebate_amount", 0.0) * p.get_discount_factor(p.discount_end_date)
+                        for p in per_rate])
+        out["price"][is_ko] = reb[rix[is_ko]]
     # Black-76 legs: vanilla rows, knocked-in rows, and knock-in parity
-    van = np.fromiter((b == "none" or b in KI_KIND for b in bts), bool, R)
+    van = ~is_ko
     if np.any(van):
         vi = np.nonzero(van)[0]
         gv = _black76_greeks(S0[vi], K[vi], sig[vi], T, carry[vi], t_carry, disc[vi], t_disc,
@@ -292,11 +303,10 @@ def result_columns(cols: Dict[str, Sequence], res: Dict[str, np.ndarray]) -> Dic
     for k in ("scenario_name", "S0", "K", "sigma", "rate", "barrier_type"):
         out[k] = list(cols[k])
     for k in ("upper_barrier", "lower_barrier"):
-        out[k] = [np.nan if v is None else v for v in _opt_col(cols, k, R)]
+        out[k] = _num_col(cols, k, R)
     for name in ("price", "delta", "gamma", "vega"):
         model = np.asarray(res[name], np.float64)
-        fa = np.array([np.nan if v is None else float(v)
-                       for v in _opt_col(cols, f"FA_{name}", R)], np.float64)
+        fa = _num_col(cols, f"FA_{name}", R)
         out[f"model_{name}"] = model
         out[f"FA_{name}"] = fa
         out[f"{name}_diff"] = np.abs(model - fa)
