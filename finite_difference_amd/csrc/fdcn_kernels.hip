@@ -375,6 +375,41 @@ __host__ __device__ constexpr bool rec_form(int it, int w, int npt) {
   return !it && w == 1 && npt > 40;
 }
 
+// Sub-chains per lane (see "chunk decomposition" in fdcn_march).
+__host__ __device__ constexpr int sub_chains(int it, int w, int npt, int zg) {
+  return (w == 1 && !(zg & 2))
+             ? (npt >= 48 ? 2 : ((it && npt == 32) ? 4 : 1))
+             : ((npt % 4 == 0 && npt >= 16) ? 4 : ((npt % 2 == 0 && npt >= 8) ? 2 : 1));
+}
+
+// Two-pass solve (the one-wave IT throughput variants): each sub-chain runs
+// its forward and its backward recurrence once with zero carries, in place;
+// the true solution differs from that by a homogeneous solution of the two
+// recurrences, C P'_i + D G_i with per-phase tables
+//   P'_i = sum_{k=i}^{M-1} bm^(k-i) fm^k,   G_i = bm^(M-i)
+// and per-sub-chain coefficients C = fm * (forward carry), D = backward
+// carry, which the carry scans deliver.  The Sherman-Morrison correction g z
+// is of the same form on every sub-chain (z's own C, D, tabulated per lane),
+// so it folds into C and D.  Two FMAs per node for the carries and the
+// correction together, where re-running both passes and correcting took
+// three, and the step's dependent chain is two passes long instead of four.
+// Measured (tools/gpu_ab.sh, two boxes): config 2 11.25 -> 11.09 ms and
+// 11.45 -> 11.21 ms per launch.  The split-form CN (config 3) lost with it:
+// its update reads two tables per node against one, and at its 128-register
+// cap the prefetch spilled (10.9 ms against 5.5; 6.0 with S = 2 at three
+// waves per SIMD), so it keeps the re-run passes.
+__host__ __device__ constexpr bool two_pass(int it, int w, int npt, int zg) {
+  return it && w == 1 && zg == 0 && npt >= 2;
+}
+
+// Doubles of the correction tables per scenario.  Two-pass variants: per
+// phase P'[M], G[M], then [lz][C z(S), D z(S)]; otherwise z itself, [2][lz][NPT+1].
+__host__ __device__ constexpr int sm_doubles(int it, int w, int npt, int zg, int lz) {
+  return two_pass(it, w, npt, zg)
+             ? 2 * (2 * (npt / sub_chains(it, w, npt, zg)) + lz * 2 * sub_chains(it, w, npt, zg))
+             : 2 * lz * (npt + 1);
+}
+
 
 // The split-form update of four slots: T_i += g z_i, V_i = s T_i - V_i (last
 // slot scaled by s_last when kLast).  s in an SGPR pair, or a VGPR (kVs:
@@ -458,7 +493,8 @@ struct Geo {
 // doubles of LDS per scenario
 template <int IT, int W, int NPT, int ZG = 0>
 __host__ __device__ inline int lds_doubles_per_scen(int lz) {
-  return ((ZG & 1) ? 0 : 2 * lz * (NPT + 1)) + (Geo<IT, W, NPT, ZG>::kPhiLds ? 64 * W * NPT : 0) +
+  return ((ZG & 1) ? 0 : sm_doubles(IT, W, NPT, ZG, lz)) +
+         (Geo<IT, W, NPT, ZG>::kPhiLds ? 64 * W * NPT : 0) +
          (W > 1 ? Xch<W>::kSize : 0) + (Geo<IT, W, NPT, ZG>::kScanLds ? kScanLdsDoubles : 0);
 }
 
@@ -517,7 +553,7 @@ fdcn_march(KArgs A) {
   double* my = lds + (size_t)scen_in_blk * lds_doubles_per_scen<IT, W, NPT, ZG>(lz);
   // SM table [2][lz][NPT+1]: LDS, or this scenario's workspace slice (ZG)
   double* ztab = (ZG & 1) ? A.zg + (size_t)scen * 2 * lz * (NPT + 1) : my;
-  double* phit = my + ((ZG & 1) ? 0 : 2 * lz * (NPT + 1));  // payoff [NPT][L] (kPhiLds)
+  double* phit = my + ((ZG & 1) ? 0 : sm_doubles(IT, W, NPT, ZG, lz));  // payoff [NPT][L] (kPhiLds)
   double* xch = phit + (kPhiLds ? L * NPT : 0);       // exchange area (W > 1)
   constexpr bool kScanLds = Geo<IT, W, NPT, ZG>::kScanLds;
   // scan weights of stages 2-5 (kScanLds), [stage-2][fwd, bwd][lane]; a paired
@@ -649,9 +685,7 @@ fdcn_march(KArgs A) {
   // IT NPT = 32 variant (config 2, two waves per SIMD) is now faster with
   // four: S = 1 11.39 ms, S = 2 11.38, S = 4 11.20; config 3 keeps one
   // (5.91 against 6.04 with four).
-  constexpr int S = (W == 1 && !(ZG & 2))
-                        ? (NPT >= 48 ? 2 : ((IT && NPT == 32) ? 4 : 1))
-                        : ((NPT % 4 == 0 && NPT >= 16) ? 4 : ((NPT % 2 == 0 && NPT >= 8) ? 2 : 1));
+  constexpr int S = sub_chains(IT, W, NPT, ZG);
   constexpr int M = NPT / S;
 
   // ---- per-theta constants: scan window products + SM table -------------
@@ -691,6 +725,26 @@ fdcn_march(KArgs A) {
   // Config 5 (NPT = 64): 26.0 -> 23.8 ms per launch against the stencil form.
   constexpr bool kRec = rec_form(IT, W, NPT);
   static_assert(!(kRec && kSplit), "one step form per variant");
+  // two-pass solve (see two_pass): tables per phase at ztab + tab * kTPh
+  constexpr bool kTP = two_pass(IT, W, NPT, ZG);
+  static_assert(!kTP || (IT && M >= 2 && !kPair), "two-pass: IT, one scenario per wave, M >= 2");
+  const int kTPh = kTP ? 2 * M + lz * 2 * S : 0;  // doubles per phase
+  // per sub-chain coefficients of the homogeneous part (two-pass solve), the
+  // solution's value at the chunk's first node after the backward scan, and
+  // per-lane phase constants: P'_0 of the last sub-chain (short lanes: one
+  // node less), the short-lane transform of the last sub-chain's D (k1, k2),
+  // the backward pass-1 multiplier into the last real node (0 on short lanes)
+  double CC[kTP ? S : 1], DD[kTP ? S : 1];
+  double cbv = 0.0, P0u = 0.0, p0l = 0.0, k1 = 0.0, k2 = 0.0, bw1l = 0.0;
+  (void)CC;
+  (void)DD;
+  (void)cbv;
+  (void)P0u;
+  (void)p0l;
+  (void)k1;
+  (void)k2;
+  (void)bw1l;
+  (void)kTPh;
   constexpr bool kNatural = IT || kSplit || kRec;  // solve input in the natural layout
   double V[NPT];
   double X = 0.0;  // node 0 of the shifted RHS layout (stencil CN; see solve)
@@ -726,6 +780,21 @@ fdcn_march(KArgs A) {
     mulLF = shrt ? fM1 : fmM;
     fmM_act = active ? fmM : 0.0;
     mulLB = shrt ? bM1 : bmM;
+    if constexpr (kTP) {
+      // P'_0 = sum_{k<M} bm^k fm^k; a short lane's last sub-chain ends one
+      // node early: P'_0 - fm^(M-1) bm^(M-1), and its backward carry enters
+      // at slot M-2, bm^(M-1-i) = G_i / bm, with its forward part
+      // -C fm^(M-1) moved over (D'' = (D - C fm^(M-1)) / bm; any D when
+      // bm = 0, where G_i vanishes on the real slots)
+      double acc = 0.0;
+#pragma unroll
+      for (int k = M - 1; k >= 0; --k) acc = fma(p.bm, acc, pow_n<NPT>(p.fm, k));
+      P0u = U(acc);
+      p0l = shrt ? P0u - fM1 * bM1 : P0u;
+      k1 = shrt ? -fM1 : 0.0;
+      k2 = shrt ? (p.bm != 0.0 ? 1.0 / p.bm : 0.0) : 1.0;
+      bw1l = shrt ? 0.0 : p.bm;
+    }
     const int len = shrt ? NPT - 1 : NPT;
     double f = active ? pow_n<NPT>(p.fm, len) : 0.0;
     double g = active ? pow_n<NPT>(p.bm, len) : 0.0;
@@ -1012,6 +1081,84 @@ fdcn_march(KArgs A) {
     }
   };
 
+  // Two-pass solve (kTP, W = 1): both zero-carry passes in place on Wr, the
+  // carries into CC / DD (see two_pass); the caller adds C P'_i + D G_i.
+  // cbv: the solution at the chunk's first node (lane 0: interior node 0).
+  auto solve_tp = [&](const Phase& p) __attribute__((always_inline)) {
+    const double fm = p.fm, bm = p.bm;
+    FDCN_PRIO_HI();
+    // forward pass 1: zero-carry values of every sub-chain, in place
+    double a[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      double w = In(j * M);
+#pragma unroll
+      for (int i = 1; i < M; ++i) {
+        const int k = j * M + i;
+        w = fma(k == NPT - 1 ? mlast : fm, w, In(k));
+        Wr(k) = w;
+      }
+      a[j] = w;
+    }
+    double e = a[0];
+#pragma unroll
+    for (int j = 1; j < S; ++j) e = fma(j == S - 1 ? mulLF : fmM, e, a[j]);
+    double b = e;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b = fma(FW[j], scan_up(b, 1 << j, lane4), b);
+    if (nst_f > 2) {
+#pragma unroll
+      for (int j = 2; j < 6; ++j) {
+        const double wf = kScanLds ? sw[(j - 2) * 128 + lane] : FW[j];
+        if (j < nst_f) b = fma(wf, scan_up(b, 1 << j, lane4), b);
+      }
+    }
+    // forward carries: into sub-chain 0 from the lane below (0 on lane 0 and
+    // dropped on inactive lanes by fm_act), then across the sub-chains
+    const double cin = shfl_up1(b, 1);
+    CC[0] = fm_act * cin;
+    double c = cin;
+#pragma unroll
+    for (int j = 1; j < S; ++j) {
+      c = fma(j == 1 ? fmM_act : fmM, c, a[j - 1]);
+      CC[j] = fm * c;
+    }
+    // backward pass 1 in place; a short lane's last real node starts its
+    // sub-chain with a zero carry (bw1l = 0)
+    FDCN_PRIO_LO();
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      double y = Wr(j * M + M - 1);
+#pragma unroll
+      for (int i = M - 2; i >= 0; --i) {
+        const int k = j * M + i;
+        y = fma(k == NPT - 2 ? bw1l : bm, y, Wr(k));
+        Wr(k) = y;
+      }
+      // the sub-chain's start value with its forward carry, zero backward carry
+      a[j] = fma(CC[j], j == S - 1 ? p0l : P0u, y);
+    }
+    FDCN_PRIO_HI();
+    e = a[S - 1];
+#pragma unroll
+    for (int j = S - 2; j >= 0; --j) e = fma(bmM, e, a[j]);
+    double cb = e;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) cb = fma(GW[j], scan_dn(cb, 1 << j, lane4), cb);
+    if (nst_b > 2) {
+#pragma unroll
+      for (int j = 2; j < 6; ++j) {
+        const double wg = kScanLds ? sw[(j - 2) * 128 + 64 + lane] : GW[j];
+        if (j < nst_b) cb = fma(wg, scan_dn(cb, 1 << j, lane4), cb);
+      }
+    }
+    cbv = cb;
+    DD[S - 1] = shfl_dn1(cb, 1);  // lane 63 receives 0
+#pragma unroll
+    for (int j = S - 2; j >= 0; --j) DD[j] = fma(j + 1 == S - 1 ? mulLB : bmM, DD[j + 1], a[j + 1]);
+  };
+  (void)solve_tp;
+
   // broadcast of the solution at interior node 0 (lane 0 of wave 0)
   auto bcast_first = [&](double v0lane) __attribute__((always_inline)) -> double {
     if constexpr (kPair) {  // lane 0 / lane 32: each scenario's own node 0
@@ -1039,6 +1186,31 @@ fdcn_march(KArgs A) {
       vb1 = 0.0;
     } else {
       Wr(0) = (t == 0) ? p.inv_r : 0.0;
+    }
+    if constexpr (kTP) {
+      solve_tp(p);
+      double* tph = ztab + tab * kTPh;
+      if (lane < M) {  // this phase's P'_i and G_i, i = lane
+        double acc = 0.0;
+#pragma unroll
+        for (int k = M - 1; k >= 0; --k)
+          if (k >= lane) acc = fma(p.bm, acc, pow_n<NPT>(p.fm, k));
+        tph[lane] = acc;
+        tph[M + lane] = pow_n<NPT>(p.bm, M - lane);
+      }
+      if (t < lz) {
+        // z on every sub-chain of this lane is C_z P' + D_z G; on lane 0's
+        // first one the input e0/r itself contributes (1/r) P'
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          tph[2 * M + t * 2 * S + j] = CC[j] + ((t == 0 && j == 0) ? p.inv_r : 0.0);
+          tph[2 * M + t * 2 * S + S + j] = DD[j];
+        }
+      }
+      // z at interior node 0 (lane 0, slot 0: no forward carry there)
+      const double d0 = (S == 1) ? k2 * fma(CC[0], k1, DD[0]) : DD[0];
+      const double z0 = bcast_first(fma(d0, bmM, fma(CC[0], P0u, Out(0))));
+      return U(p.kappa / (1.0 + p.kappa * z0));
     }
     solve(p, std::false_type{});
     if (t < lz) {
@@ -1392,6 +1564,80 @@ fdcn_march(KArgs A) {
     if (shrt) V[NPT - 2] = 0.0;  // the phantom node's rhs
     }  // CN rhs
 
+    if constexpr (kTP) {
+      // ---- 2. two-pass solve; Sherman-Morrison folded into the carries ----
+      solve_tp(ph);
+      const double g = smc_l * read_lane(cbv, 0);
+      const int tb = opaque(tab * kTPh);  // this phase's tables
+      {
+        const double* zr = ztab + tb + 2 * M + (t < lz ? t : lz - 1) * 2 * S;
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          CC[j] = fma(g, zr[j], CC[j]);
+          DD[j] = fma(g, zr[S + j], DD[j]);
+        }
+      }
+      DD[S - 1] = k2 * fma(CC[S - 1], k1, DD[S - 1]);  // short lanes (see setup_scan)
+      // ---- 3. x = Wr + C P'_i + D G_i and the step's update ---------------
+      // nodes in (slot i, sub-chain j) order, four at a time: a slot's two
+      // table values (LDS broadcasts) serve all S sub-chains
+      __builtin_amdgcn_s_setprio(1);
+      const double cq = (m + 1 < A.n_ranna) ? 1.0 : 2.0;  // 1/theta of the next step
+      const int poff = opaque(t);
+      // node of the u-th entry of group q: slot (q+u)/S of sub-chain (q+u)%S
+#define FDCN_TP_K(u) ((((q) + (u)) % S) * M + ((q) + (u)) / S)
+      // the tables one group ahead of their use (LDS latency under the
+      // previous group's arithmetic)
+      double tpn[4], tgn[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        tpn[u] = ztab[tb + u / S];
+        tgn[u] = ztab[tb + M + u / S];
+      }
+#pragma unroll
+      for (int q = 0; q < NPT; q += 4) {
+        double tpc[4], tgc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          tpc[u] = tpn[u];
+          tgc[u] = tgn[u];
+        }
+        if (q + 4 < NPT) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            tpn[u] = ztab[tb + (q + 4 + u) / S];
+            tgn[u] = ztab[tb + M + (q + 4 + u) / S];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = (q + u) % S;
+          V[FDCN_TP_K(u)] = fma(DD[j], tgc[u], fma(CC[j], tpc[u], V[FDCN_TP_K(u)]));
+        }
+        // the Ikonen-Toivanen update (W, V', Q'; see the re-run form below)
+        double pk[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pk[u] = phit[poff + FDCN_TP_K(u) * L];
+        asm volatile(
+            "v_fma_f64 %4, %12, %0, -%4\n\t"
+            "v_fma_f64 %5, %12, %1, -%5\n\t"
+            "v_fma_f64 %6, %12, %2, -%6\n\t"
+            "v_fma_f64 %7, %12, %3, -%7\n\t"
+            "v_max_f64 %0, %8, %4\n\t"
+            "v_max_f64 %1, %9, %5\n\t"
+            "v_max_f64 %2, %10, %6\n\t"
+            "v_max_f64 %3, %11, %7\n\t"
+            "v_fma_f64 %4, %13, %0, -%4\n\t"
+            "v_fma_f64 %5, %13, %1, -%5\n\t"
+            "v_fma_f64 %6, %13, %2, -%6\n\t"
+            "v_fma_f64 %7, %13, %3, -%7"
+            : "+v"(V[FDCN_TP_K(0)]), "+v"(V[FDCN_TP_K(1)]), "+v"(V[FDCN_TP_K(2)]),
+              "+v"(V[FDCN_TP_K(3)]), "+v"(QS[FDCN_TP_K(0)]), "+v"(QS[FDCN_TP_K(1)]),
+              "+v"(QS[FDCN_TP_K(2)]), "+v"(QS[FDCN_TP_K(3)])
+            : "v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]), "s"(ph.inv_r), "s"(cq));
+      }
+#undef FDCN_TP_K
+    } else {
     // ---- 2. tridiagonal solve ---------------------------------------------
     if constexpr (kRec) {
       // one fused solve for both phases (a second, plain solve for the
@@ -1541,6 +1787,7 @@ fdcn_march(KArgs A) {
         }
       }
     }
+    }  // !kTP
     if constexpr (!IT && !kTabSplit) {  // IT and kTabSplit read tabulated terms instead
       V0 = lo_new;
       VN = hi_new;
