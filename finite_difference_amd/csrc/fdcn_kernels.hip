@@ -29,9 +29,6 @@
 //      only the first K nodes (K = extent where it drops below 1e-18 z_0)
 //      are touched.  This is the reference's Thomas solve in exact
 //      arithmetic (discrete_barrier_fdm_pricer.py:487-509), reassociated.
-//      The one-wave IT variants instead run each pass once and add the
-//      carries' and the correction's homogeneous solution from tables
-//      (two_pass below).
 //   3. Write Dirichlet values, then knock-out projection on monitor steps
 //      (integer node thresholds) or the Ikonen-Toivanen update (lambda and
 //      the payoff in VGPR/LDS).
