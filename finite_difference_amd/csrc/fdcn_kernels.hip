@@ -734,7 +734,7 @@ fdcn_march(KArgs A) {
   // per-lane phase constants: P'_0 of the last sub-chain (short lanes: one
   // node less), the short-lane transform of the last sub-chain's D (k1, k2),
   // the backward pass-1 multiplier into the last real node (0 on short lanes)
-  double CC[kTP ? S : 1], DD[kTP ? S : 1];
+  double CC[S], DD[S];  // kTP only (unused arrays vanish elsewhere)
   double cbv = 0.0, P0u = 0.0, p0l = 0.0, k1 = 0.0, k2 = 0.0, bw1l = 0.0;
   (void)CC;
   (void)DD;
@@ -1420,7 +1420,15 @@ fdcn_march(KArgs A) {
     halo_l = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
     halo_r = shfl_dn1(V[0], 1);
   }
-  for (int m = 0; m < A.n_time; ++m) {
+  // Steps in blocks of kStride: a block's boundary terms (one step per lane)
+  // stay in bnd_cur for the whole block while the next block's load is in
+  // flight.  With the refill inside a flat step loop the compiler rotated the
+  // two buffers through copies on every step (8 v_mov_b64 per step).
+  for (int m0 = 0; m0 < A.n_time; m0 += kStride) {
+    bnd_cur = bnd_nxt;
+    if (m0 + kStride < A.n_pad) bnd_nxt = bnd[m0 + kStride + hl];  // prefetch the block after
+    const int m_end = min(m0 + kStride, A.n_time);
+  for (int m = m0; m < m_end; ++m) {
     if (m == A.n_ranna && use_r) {  // Rannacher -> Crank-Nicolson
       if constexpr (kPair) {
         // reloaded rather than kept live through the march (VGPRs, per lane)
@@ -1435,10 +1443,6 @@ fdcn_march(KArgs A) {
       smc_l = sm_row * smc;
       s_l = shrt ? 0.0 : ph.s;
       tab = 1;
-    }
-    if ((m & (kStride - 1)) == 0) {  // Dirichlet values of the next steps, one per lane
-      bnd_cur = bnd_nxt;
-      if (m + kStride < A.n_pad) bnd_nxt = bnd[m + kStride + hl];  // prefetch the block after
     }
     // kSplit: the tabulated rhs terms; kPair: each scenario's from its own lanes
     double lo_new = kPair ? (half ? read_lane(bnd_cur.x, 32 + (m & 31)) : read_lane(bnd_cur.x, m & 31))
@@ -1476,8 +1480,10 @@ fdcn_march(KArgs A) {
         const int kb = kPair ? ((ko_prev >> (2 * half)) & 3) : ko_prev;
         const double2 raw = bnd_raw[m];  // the step's raw Dirichlet values
         const double rlo = U(raw.x), rhi = U(raw.y);
-        if (kb & 1) blo = ph.th * (ph.pl * fma(ph.c2, V0, rlo));
-        if (kb & 2) bhi = ph.th * (ph.pu * fma(ph.c2, VN, rhi));
+        // (uniform: kept in SGPRs like the tabulated terms, so the merge
+        // after this branch needs no VGPR copies on the common path)
+        if (kb & 1) blo = U(ph.th * (ph.pl * fma(ph.c2, V0, rlo)));
+        if (kb & 2) bhi = U(ph.th * (ph.pu * fma(ph.c2, VN, rhi)));
         ko_prev = 0;
       }
       vb0 = fma(e_first, blo, V[0]);
@@ -1904,7 +1910,8 @@ fdcn_march(KArgs A) {
       halo_l = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
       halo_r = shfl_dn1(V[0], 1);
     }
-  }
+  }  // step
+  }  // block of kStride steps
 
   if constexpr (IT) {  // Dirichlet values of the last step (the loop kept only rhs terms)
     if (A.n_time > 0) {
