@@ -336,11 +336,13 @@ struct MonRun {
 };
 
 // Each wave's workspace row ends in kKoRow double2 = 64 per-slot knock-out
-// masks.  For NPT >= 48 the NPT masks (2 NPT SGPRs) do not fit the scalar
-// file: the compiler spilled them to VGPR lanes and read each back with two
-// v_readlane per slot and monitor step.  Those variants store the masks
-// once (vector stores) and reload them per monitor step with s_load, which
-// costs no VALU issue.
+// masks.  From NPT = 16 on the NPT masks (2 NPT SGPRs) do not fit the scalar
+// file next to everything else: the compiler spilled them to VGPR lanes and
+// read each back with two v_readlane per slot and monitor step (four VALU
+// per slot with the two v_cndmask).  Those variants store the masks once
+// (vector stores) and reload them per monitor step with s_load: one
+// exec-masked v_mov_b64 per slot.  (NPT = 16 joined in round 2: config 3,
+// daily monitoring, 4 VALU per wave and step fewer on average.)
 constexpr int kKoRow = 32;
 typedef unsigned KoMask16 __attribute__((ext_vector_type(16)));  // 8 masks, s_load_dwordx16
 __device__ __forceinline__ unsigned long long ko_pair(KoMask16 m, int j) {
@@ -348,7 +350,7 @@ __device__ __forceinline__ unsigned long long ko_pair(KoMask16 m, int j) {
 }
 template <int IT, int NPT, int ZG = 0>
 struct KoLoad {  // also the paired flavour: two scenarios' masks would crowd the scalar file
-  static constexpr bool value = !IT && (NPT >= 48 || (ZG & 4));
+  static constexpr bool value = !IT && ((NPT >= 16 && NPT % 8 == 0) || (ZG & 4));
 };
 
 // CN variants marched in the split form (state V, solve into T; see the step
@@ -1804,9 +1806,9 @@ fdcn_march(KArgs A) {
       const double reb = kPair ? (half ? mon2.cur : mon.cur) : mon.cur;
       double rebv = reb;  // VGPR copy: v_cndmask takes the mask as its SGPR operand
       asm volatile("" : "+v"(rebv));
-      // NPT <= 40: the per-slot masks are loop-invariant, the compiler
-      // hoists them and they stay in SGPRs.  NPT >= 48 (KoLoad): they would
-      // spill to VGPR lanes (two v_readlane per slot), so they are reloaded
+      // Short chunks: the per-slot masks are loop-invariant, the compiler
+      // hoists them and they stay in SGPRs.  KoLoad variants (NPT >= 16):
+      // they would spill to VGPR lanes (two v_readlane per slot), so they are reloaded
       // from the workspace row with s_load_dwordx16 and applied as one
       // exec-masked v_mov_b64 per slot (config 5: 29.3 -> 26.0 ms per
       // launch).  Rebuilding the masks on the scalar unit from (full, part,
