@@ -505,7 +505,7 @@ __host__ __device__ inline int lds_doubles_per_scen(int lz) {
 // scan, the carries), then pass 2.  Raised priority over pass 1 + scan lets
 // a wave reach its carries first while the other wave of its SIMD streams
 // the independent FMAs of its own pass 2 / update and fills the gaps.
-// Measured (tools/gpu_ab_n.sh): scans only: config 2 12.44 -> 12.22 ms,
+// Measured (tools/gpu_ab.sh): scans only: config 2 12.44 -> 12.22 ms,
 // config 3 6.66 -> 6.46 ms, config 5 unchanged; pass 1 + scan (this) a
 // further -1.3 / -2.2 % on config 2 (two boxes), -0.6 % on config 5, config
 // 3 neutral; raising it over the Sherman-Morrison broadcast lost time.
@@ -679,7 +679,7 @@ fdcn_march(KArgs A) {
   // their carries cost 2(S-1) FMAs per sweep and lane.  With the priority
   // scheme above, the throughput variants (W = 1, 2-3 waves per SIMD) hide
   // the FMA latency with the other waves: one chain (S = 1) measured
-  // fastest up to 40 nodes per lane, two at 48-64 (tools/gpu_ab_n.sh: config
+  // fastest up to 40 nodes per lane, two at 48-64 (tools/gpu_ab.sh: config
   // 2 12.31 -> 12.08 ms, config 3 6.54 -> 6.21 ms, config 5 20.65 -> 19.69 ms
   // against S = 4).  The multi-wave variants serve small batches, where one
   // wave per SIMD needs the in-wave ILP: they keep 4.  Re-measured in round 2
@@ -1706,7 +1706,7 @@ fdcn_march(KArgs A) {
     // IT and kRec: the update / knock-out and the next RHS at priority 1,
     // between pass 1 + scan (3) and pass 2 (0): config 2 11.99 -> 11.74 ms,
     // config 5 19.73 -> 18.41 ms (3 instead of 1: 18.65); kSplit lost 2 %
-    // with it (tools/gpu_ab_n.sh)
+    // with it (tools/gpu_ab.sh)
     if constexpr (IT || kRec) __builtin_amdgcn_s_setprio(1);
     const double cq = (m + 1 < A.n_ranna) ? 1.0 : 2.0;  // 1/theta of the next step (IT)
     (void)cq;
@@ -2002,7 +2002,7 @@ Variant mk() {
 
 // The paired flavour (CN split form) for grids of up to 256 interior nodes,
 // against one scenario per wave at 4 nodes per lane.  Measured on the
-// config-3 batch (10 000 scenarios x 2000 steps, tools/gpu_pair_ab.sh):
+// config-3 batch (10 000 scenarios x 2000 steps, tools/gpu_ab.sh with FDCN_VARIANT; profiles/r02_pair_ab/):
 // 256 nodes 3.26 -> 2.94 ms; but 512 nodes 4.35 -> 4.96 (NPT 8 vs paired
 // 16) and 1024 nodes 5.81 -> 6.76 (NPT 16 vs paired 32): the paired waves'
 // per-lane constants push them to 176 / 242 VGPRs, two waves per SIMD where
