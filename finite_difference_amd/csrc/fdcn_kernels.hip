@@ -348,9 +348,14 @@ typedef unsigned KoMask16 __attribute__((ext_vector_type(16)));  // 8 masks, s_l
 __device__ __forceinline__ unsigned long long ko_pair(KoMask16 m, int j) {
   return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];
 }
-template <int IT, int NPT, int ZG = 0>
+// Only the one-wave throughput variants reload from NPT = 16 on: the latency
+// variants (several waves, or the single-trade flavour) have a knock-out on
+// the critical path of one trade, where the s_load latency of every monitor
+// step showed (config 5 trade, every step: 12.5 -> 14.0 ms).
+template <int IT, int W, int NPT, int ZG = 0>
 struct KoLoad {  // also the paired flavour: two scenarios' masks would crowd the scalar file
-  static constexpr bool value = !IT && ((NPT >= 16 && NPT % 8 == 0) || (ZG & 4));
+  static constexpr bool value =
+      !IT && (NPT >= 48 || (W == 1 && !(ZG & 2) && NPT >= 16 && NPT % 8 == 0) || (ZG & 4));
 };
 
 // CN variants marched in the split form (state V, solve into T; see the step
@@ -1321,7 +1326,7 @@ fdcn_march(KArgs A) {
   (void)shrt_ballot;
   unsigned long long kom_addr = 0;  // this wave's mask row (KoLoad variants)
   unsigned long long kom_addr2 = 0, kom_addr12 = 0;  // kPair: second scenario's / both
-  if constexpr (KoLoad<IT, NPT, ZG>::value) {
+  if constexpr (KoLoad<IT, W, NPT, ZG>::value) {
     unsigned long long* kom = reinterpret_cast<unsigned long long*>(bnd + A.n_pad);
     // kRec / kSplit keep the phantom slot of short lanes at zero: never knock it out
     const unsigned long long shrt_lanes = (kRec || kSplit) ? (unsigned long long)__ballot(shrt) : 0ull;
@@ -1813,7 +1818,7 @@ fdcn_march(KArgs A) {
       // exec-masked v_mov_b64 per slot (config 5: 29.3 -> 26.0 ms per
       // launch).  Rebuilding the masks on the scalar unit from (full, part,
       // k0, k1) measured slower still (34.8 ms): five SALU per slot.
-      if constexpr (KoLoad<IT, NPT, ZG>::value) {
+      if constexpr (KoLoad<IT, W, NPT, ZG>::value) {
         // eight slots per block: each slot is one v_mov_b64 of the rebate
         // under an exec mask set on the scalar unit (s_and_b64 with the
         // saved exec), while the next block's eight masks arrive (one

@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 \
     --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py > $O/bench_american.json 2> $O/bench_american.err || exit $?
-for wl in barrier double analytic scenario_file trade_cnlog trade_american trade_double; do
+for wl in barrier double analytic scenario_file american_file trade_cnlog trade_american trade_double; do
   timeout -k 10 300 python bench.py --workload $wl > $O/bench_$wl.json 2> $O/bench_$wl.err || exit $?
 done
 for wl in american barrier double; do
@@ -20,3 +20,7 @@ for wl in american barrier double; do
       python3 bench.py --workload $wl --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_$wl.log 2>&1 || exit $?
 done
 bash tools/pmc_counters.sh ${TAG}_pmc american barrier double || exit $?
+# the launcher path the driver's scaling run uses (one rank here: one GPU)
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 1 --no-cpu-baseline \
+    > $O/bench_torchrun_n1.json 2> $O/bench_torchrun_n1.err || exit $?
