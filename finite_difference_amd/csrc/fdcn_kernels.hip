@@ -1418,8 +1418,13 @@ fdcn_march(KArgs A) {
   smc_l = sm_row * smc;
   s_l = shrt ? 0.0 : ph.s;
 
+  // The register-capped config-3 variant loads each block when it starts:
+  // a prefetched next block spilled to scratch there (16 B per lane and
+  // block out and back in: +170 MB of HBM traffic per launch).
+  constexpr bool kBndPrefetch = kWavesPerEu<IT, W, NPT, ZG> == 1;
   double2 bnd_cur = make_double2(0.0, 0.0);
-  double2 bnd_nxt = bnd[hl];  // steps 0..kStride-1
+  double2 bnd_nxt = kBndPrefetch ? bnd[hl] : make_double2(0.0, 0.0);  // steps 0..kStride-1
+  (void)bnd_nxt;
   int ko_prev = 0;  // kSplit: bit 0 / 1 -- the last step knocked out node 0 / the last node
   (void)ko_prev;
   double halo_l = 0.0, halo_r = 0.0;
@@ -1432,8 +1437,12 @@ fdcn_march(KArgs A) {
   // flight.  With the refill inside a flat step loop the compiler rotated the
   // two buffers through copies on every step (8 v_mov_b64 per step).
   for (int m0 = 0; m0 < A.n_time; m0 += kStride) {
-    bnd_cur = bnd_nxt;
-    if (m0 + kStride < A.n_pad) bnd_nxt = bnd[m0 + kStride + hl];  // prefetch the block after
+    if constexpr (kBndPrefetch) {
+      bnd_cur = bnd_nxt;
+      if (m0 + kStride < A.n_pad) bnd_nxt = bnd[m0 + kStride + hl];  // prefetch the block after
+    } else {
+      bnd_cur = bnd[m0 + hl];
+    }
     const int m_end = min(m0 + kStride, A.n_time);
   for (int m = m0; m < m_end; ++m) {
     if (m == A.n_ranna && use_r) {  // Rannacher -> Crank-Nicolson
