@@ -495,6 +495,12 @@ struct Geo {
   // one-wave CN variants keep the weights of scan stages 2-5 in LDS (see
   // setup_scan); IT's LDS already holds the payoff
   static constexpr bool kScanLds = !IT && W == 1;
+  // the current 64-step block of boundary terms, one double2 per step and
+  // wave, read back as an LDS broadcast each step instead of four
+  // v_readlane: CN only (A/B: config 3 5.25 -> 5.18 ms, config 5 18.43 ->
+  // 18.35; IT, two waves per SIMD with the payoff in LDS, 11.08 -> 11.17),
+  // not the paired flavour, whose halves read different scenarios' terms
+  static constexpr bool kBndLds = !IT && !(ZG & 4);
 };
 
 // doubles of LDS per scenario
@@ -502,7 +508,8 @@ template <int IT, int W, int NPT, int ZG = 0>
 __host__ __device__ inline int lds_doubles_per_scen(int lz) {
   return ((ZG & 1) ? 0 : sm_doubles(IT, W, NPT, ZG, lz)) +
          (Geo<IT, W, NPT, ZG>::kPhiLds ? 64 * W * NPT : 0) +
-         (W > 1 ? Xch<W>::kSize : 0) + (Geo<IT, W, NPT, ZG>::kScanLds ? kScanLdsDoubles : 0);
+         (W > 1 ? Xch<W>::kSize : 0) + (Geo<IT, W, NPT, ZG>::kScanLds ? kScanLdsDoubles : 0) +
+         (Geo<IT, W, NPT, ZG>::kBndLds ? 128 * W : 0);
 }
 
 // Issue priority of the zero-carry passes and the carry scans.  Each sweep
@@ -569,6 +576,12 @@ fdcn_march(KArgs A) {
                (kPair ? 2 * lds_doubles_per_scen<IT, W, NPT, ZG>(lz) - kScanLdsDoubles : 0);
   (void)sw;
   (void)xch;
+  // this wave's block of boundary terms (kBndLds): after the scan weights
+  constexpr bool kBndLds = Geo<IT, W, NPT, ZG>::kBndLds;
+  double2* bblk = reinterpret_cast<double2*>(
+                      xch + (W > 1 ? Xch<W>::kSize : 0) + (kScanLds ? kScanLdsDoubles : 0)) +
+                  (kBndLds ? wave * 64 : 0);
+  (void)bblk;
 
   const double* P = A.params + (size_t)scen * FDCN_NPARAM;
   const int32_t* I = A.iparams + (size_t)scen * FDCN_NIPARAM;
@@ -1443,6 +1456,13 @@ fdcn_march(KArgs A) {
     } else {
       bnd_cur = bnd[m0 + hl];
     }
+    if constexpr (kBndLds) {
+      // into LDS: each step then reads its terms as one broadcast (an LDS
+      // instruction) instead of four v_readlane (VALU); the wave's LDS
+      // operations complete in order, so no wait is needed before the reads
+      bblk[lane] = bnd_cur;
+      asm volatile("" ::: "memory");
+    }
     const int m_end = min(m0 + kStride, A.n_time);
   for (int m = m0; m < m_end; ++m) {
     if (m == A.n_ranna && use_r) {  // Rannacher -> Crank-Nicolson
@@ -1461,10 +1481,17 @@ fdcn_march(KArgs A) {
       tab = 1;
     }
     // kSplit: the tabulated rhs terms; kPair: each scenario's from its own lanes
-    double lo_new = kPair ? (half ? read_lane(bnd_cur.x, 32 + (m & 31)) : read_lane(bnd_cur.x, m & 31))
-                          : read_lane(bnd_cur.x, m & 63);
-    double hi_new = kPair ? (half ? read_lane(bnd_cur.y, 32 + (m & 31)) : read_lane(bnd_cur.y, m & 31))
-                          : read_lane(bnd_cur.y, m & 63);
+    double lo_new, hi_new;
+    if constexpr (kBndLds) {
+      const double2 bt = bblk[m - m0];
+      lo_new = bt.x;
+      hi_new = bt.y;
+    } else {  // kPair: each scenario's from its own lanes
+      lo_new = kPair ? (half ? read_lane(bnd_cur.x, 32 + (m & 31)) : read_lane(bnd_cur.x, m & 31))
+                     : read_lane(bnd_cur.x, m & 63);
+      hi_new = kPair ? (half ? read_lane(bnd_cur.y, 32 + (m & 31)) : read_lane(bnd_cur.y, m & 31))
+                     : read_lane(bnd_cur.y, m & 63);
+    }
 
     // ---- 1. rhs ------------------------------------------------------------
     if constexpr (IT) {
