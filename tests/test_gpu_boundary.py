@@ -182,10 +182,12 @@ def test_host_entry_points_are_reentrant():
     assert not errors, errors
 
 
-def test_sharded_runner_binds_the_rank_device():
-    """run_all_scenarios through the rank code path at world size 1 (gloo
-    group on 127.0.0.1): LOCAL_RANK's GPU is selected for libfdcn and the
-    rows equal the plain run."""
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_sharded_runner_binds_the_rank_device(backend):
+    """run_all_scenarios through the rank code path at world size 1 (a gloo
+    or an RCCL group on 127.0.0.1; RCCL is what the 8-GPU run uses for the
+    result gather): LOCAL_RANK's GPU is selected for libfdcn and the rows
+    equal the plain run."""
     import torch.distributed as dist
     cfg = os.path.join(HERE, "golden", "ref_csv", "config_scenarios_space_1.csv")
     base = scenarios.runner_base_params("put", 60)
@@ -195,7 +197,7 @@ def test_sharded_runner_binds_the_rank_device():
     port = s.getsockname()[1]
     s.close()
     os.environ["LOCAL_RANK"] = "0"
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     try:
         from finite_difference_amd import distributed
         assert distributed.bind_device() == 0
