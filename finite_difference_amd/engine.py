@@ -13,6 +13,7 @@ to the pricers (tests use this to drive the CPU oracle as a checker).
 """
 from __future__ import annotations
 
+import threading
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -74,7 +75,7 @@ class Solve:
     lower: Boundary
     upper: Boundary
     tau0: float = 0.0
-    tau_accumulate: bool = False         # oracle-only fidelity flag (FDCN_I_TAU_MODE)
+    tau_accumulate: bool = False         # FDCN_I_TAU_MODE = 1: tau += dt per step (American loop)
     payoff: Optional[np.ndarray] = None  # IT only, [n_nodes]
     ko_lo: int = -1                      # nodes j <= ko_lo knocked out on monitor steps
     ko_hi: int = 1 << 30                 # nodes j >= ko_hi knocked out
@@ -240,6 +241,23 @@ class HipBackend:
                              g.mon_step, g.mon_rebate)
 
 
+_pool = None
+_pool_lock = threading.Lock()
+
+
+def _launch_pool():
+    """The process-wide launch threads.  libfdcn keeps one HIP stream per
+    calling thread and device for the thread's lifetime, so the threads that
+    issue concurrent launches are kept rather than created per call: a pool
+    per call would leave a stream behind with every thread it retired."""
+    global _pool
+    with _pool_lock:
+        if _pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            _pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="fdcn-launch")
+        return _pool
+
+
 class Engine:
     """Batches solves into launches on a backend (default: the HIP library).
 
@@ -259,14 +277,12 @@ class Engine:
     def _run_groups(self, groups: List[Group]) -> List[np.ndarray]:
         if len(groups) < 2 or not self.concurrent or not isinstance(self.backend, HipBackend):
             return [self.backend.run_group(g) for g in groups]
-        from concurrent.futures import ThreadPoolExecutor
         dev = capi.current_device()  # the HIP device is per thread: carry it over
 
         def one(g: Group) -> np.ndarray:
             capi.select_device(dev)
             return self.backend.run_group(g)
-        with ThreadPoolExecutor(max_workers=min(len(groups), 8)) as ex:
-            return list(ex.map(one, groups))
+        return list(_launch_pool().map(one, groups))
 
     @property
     def on_device(self) -> bool:

@@ -118,7 +118,10 @@ int fdcn_it_batch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
  * thread gets its own non-blocking HIP stream on the current device
  * (fdcn_select_device / hipSetDevice), device buffers come stream-ordered
  * from the device's memory pool, and the call waits on its own stream only
- * (never a device-wide synchronisation). */
+ * (never a device-wide synchronisation).  The stream is created on a thread's
+ * first call and kept for the thread's lifetime (it is not released when the
+ * thread exits): issue calls from long-lived threads (a fixed pool), not from
+ * a thread created per call. */
 
 /* ---- device-pointer entry points (all pointers are device memory) ----- */
 /* `stream` is a hipStream_t (NULL = default stream); the call is

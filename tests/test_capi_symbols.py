@@ -116,3 +116,37 @@ def test_select_device_without_gpu_is_an_error_not_a_crash():
         pytest.skip("GPU host")
     rc = capi.lib().fdcn_select_device(0)
     assert rc != 0
+
+
+def test_concurrent_groups_reuse_the_launch_threads():
+    """Engine.run issues groups of different shapes from the process-wide
+    launch pool (libfdcn keeps one stream per calling thread): repeated runs
+    reuse the same threads instead of creating new ones each call."""
+    import threading
+
+    import numpy as np
+
+    from finite_difference_amd import capi, engine
+
+    class Recording(engine.HipBackend):  # takes the concurrent path, no GPU call
+        def __init__(self):
+            self.threads = set()
+
+        def run_group(self, g):
+            self.threads.add(threading.get_ident())
+            return g.v_init * 2.0
+
+    solves = [engine.Solve(it=False, n_time=4, n_ranna=0, dt=0.01, coeffs=(1.0, 1.0, -2.0),
+                           v_init=np.full(n, float(n)), lower=engine.Boundary(),
+                           upper=engine.Boundary()) for n in (16, 32, 48)]
+    be = Recording()
+    eng = engine.Engine(backend=be)
+    saved = capi.current_device, capi.select_device
+    capi.current_device, capi.select_device = (lambda: 0), (lambda d: None)
+    try:
+        for _ in range(20):
+            out = eng.run(solves)
+            assert [float(o[0]) for o in out] == [32.0, 64.0, 96.0]
+    finally:
+        capi.current_device, capi.select_device = saved
+    assert 1 <= len(be.threads) <= 8
