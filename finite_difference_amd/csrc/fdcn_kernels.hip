@@ -1419,9 +1419,13 @@ fdcn_march(KArgs A) {
   // this lane's row of the correction tables (lanes >= lz read row lz-1)
   const int zoff_r = (t < lz ? t : lz - 1) * (NPT + 1);
   const int zoff_c = zoff_r + lz * (NPT + 1);
+  // the current phase's row offset, kept across steps (re-deriving it from
+  // the lane's row index took three VALU per step)
+  int zoff_cur = zoff_c;
   if (use_r) {
     smc = smc_r;
     tab = 0;
+    zoff_cur = zoff_r;
   } else {
     ph = make_phase<kPair>(0.5, dt, ca, cc, cbc);
     setup_scan(ph);
@@ -1479,6 +1483,7 @@ fdcn_march(KArgs A) {
       smc_l = sm_row * smc;
       s_l = shrt ? 0.0 : ph.s;
       tab = 1;
+      zoff_cur = zoff_c;
     }
     // kSplit: the tabulated rhs terms; kPair: each scenario's from its own lanes
     double lo_new, hi_new;
@@ -1733,7 +1738,7 @@ fdcn_march(KArgs A) {
       }
       g = smc_l * y0;
       // lane-major rows, stride NPT+1: bank-spread, immediate offsets
-      zoff = opaque(tab ? zoff_c : zoff_r);
+      zoff = opaque(zoff_cur);
     }
     if constexpr (kSplit) {
       // x = s (T + g z) - c2 V: c2 = 1 for theta = 1/2; the Rannacher steps
