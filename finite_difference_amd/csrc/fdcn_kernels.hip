@@ -89,6 +89,23 @@ __device__ __forceinline__ int opaque(int i) {
   return i;
 }
 
+// LDS byte addresses kept in a VGPR across steps.  Hiding an index makes the
+// compiler rebuild the address from it on every step (a copy, a shift-add
+// and an add); a loop-carried address passed through the asm in place
+// (a = hide_addr(a)) costs no instruction, and every load off it uses the
+// ds_read immediate offset.
+typedef __attribute__((address_space(3))) const double lds_cf64;
+__device__ __forceinline__ unsigned lds_addr(const double* p) {
+  return (unsigned)(uintptr_t)(lds_cf64*)p;
+}
+__device__ __forceinline__ double lds_ld(unsigned a, int off) {
+  return ((lds_cf64*)(uintptr_t)a)[off];
+}
+__device__ __forceinline__ unsigned hide_addr(unsigned a) {
+  asm volatile("" : "+v"(a));
+  return a;
+}
+
 // Cross-lane moves.  Shifts by one lane use the GFX9 wavefront DPP shifts
 // (wave_shr:1 / wave_shl:1: two VALU moves, no LDS round trip), by two lanes
 // two of them; longer shifts go through ds_bpermute.  Lanes without a source
@@ -1411,7 +1428,6 @@ fdcn_march(KArgs A) {
   }
   // phase for step 0 (ph currently holds the theta the last table was built for)
   double smc;
-  int tab;
   // -smc on the lanes that hold table rows, 0 elsewhere: g = smc_l y0 needs
   // no lane select
   const double sm_row = (t < lz) ? -1.0 : 0.0;
@@ -1422,15 +1438,31 @@ fdcn_march(KArgs A) {
   // the current phase's row offset, kept across steps (re-deriving it from
   // the lane's row index took three VALU per step)
   int zoff_cur = zoff_c;
+  // its LDS byte address when the table is in LDS (hide_addr)
+  constexpr bool kZLds = !(ZG & 1);
+  unsigned z_a = kZLds ? lds_addr(ztab + zoff_c) : 0u;
+  (void)z_a;
+  // kTP: LDS byte addresses of this phase's tables, of this lane's row of
+  // the Sherman-Morrison coefficients and of its payoff column (hide_addr)
+  auto tp_tab_addr = [&](int tb_) { return kTP ? lds_addr(ztab + tb_ * kTPh) : 0u; };
+  auto tp_row_addr = [&](int tb_) {
+    return kTP ? lds_addr(ztab + tb_ * kTPh + 2 * M + (t < lz ? t : lz - 1) * 2 * S) : 0u;
+  };
+  unsigned tp_ta = tp_tab_addr(1), tp_za = tp_row_addr(1);
+  unsigned tp_pa = (kTP && kPhiLds) ? lds_addr(phit + t) : 0u;
+  (void)tp_ta;
+  (void)tp_za;
+  (void)tp_pa;
   if (use_r) {
     smc = smc_r;
-    tab = 0;
     zoff_cur = zoff_r;
+    if constexpr (kZLds) z_a = lds_addr(ztab + zoff_r);
+    tp_ta = tp_tab_addr(0);
+    tp_za = tp_row_addr(0);
   } else {
     ph = make_phase<kPair>(0.5, dt, ca, cc, cbc);
     setup_scan(ph);
     smc = smc_c;
-    tab = 1;
   }
   smc_l = sm_row * smc;
   s_l = shrt ? 0.0 : ph.s;
@@ -1482,8 +1514,10 @@ fdcn_march(KArgs A) {
       smc = smc_c;
       smc_l = sm_row * smc;
       s_l = shrt ? 0.0 : ph.s;
-      tab = 1;
       zoff_cur = zoff_c;
+      if constexpr (kZLds) z_a = lds_addr(ztab + zoff_c);
+      tp_ta = tp_tab_addr(1);
+      tp_za = tp_row_addr(1);
     }
     // kSplit: the tabulated rhs terms; kPair: each scenario's from its own lanes
     double lo_new, hi_new;
@@ -1622,14 +1656,12 @@ fdcn_march(KArgs A) {
       // ---- 2. two-pass solve; Sherman-Morrison folded into the carries ----
       solve_tp(ph);
       const double g = smc_l * read_lane(cbv, 0);
-      const int tb = opaque(tab * kTPh);  // this phase's tables
-      {
-        const double* zr = ztab + tb + 2 * M + (t < lz ? t : lz - 1) * 2 * S;
+      tp_ta = hide_addr(tp_ta);  // this phase's tables
+      tp_za = hide_addr(tp_za);
 #pragma unroll
-        for (int j = 0; j < S; ++j) {
-          CC[j] = fma(g, zr[j], CC[j]);
-          DD[j] = fma(g, zr[S + j], DD[j]);
-        }
+      for (int j = 0; j < S; ++j) {
+        CC[j] = fma(g, lds_ld(tp_za, j), CC[j]);
+        DD[j] = fma(g, lds_ld(tp_za, S + j), DD[j]);
       }
       DD[S - 1] = k2 * fma(CC[S - 1], k1, DD[S - 1]);  // short lanes (see setup_scan)
       // ---- 3. x = Wr + C P'_i + D G_i and the step's update ---------------
@@ -1637,7 +1669,7 @@ fdcn_march(KArgs A) {
       // table values (LDS broadcasts) serve all S sub-chains
       __builtin_amdgcn_s_setprio(1);
       const double cq = (m + 1 < A.n_ranna) ? 1.0 : 2.0;  // 1/theta of the next step
-      const int poff = opaque(t);
+      tp_pa = hide_addr(tp_pa);
       // node of the u-th entry of group q: slot (q+u)/S of sub-chain (q+u)%S
 #define FDCN_TP_K(u) ((((q) + (u)) % S) * M + ((q) + (u)) / S)
       // the tables one group ahead of their use (LDS latency under the
@@ -1645,8 +1677,8 @@ fdcn_march(KArgs A) {
       double tpn[4], tgn[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        tpn[u] = ztab[tb + u / S];
-        tgn[u] = ztab[tb + M + u / S];
+        tpn[u] = lds_ld(tp_ta, u / S);
+        tgn[u] = lds_ld(tp_ta, M + u / S);
       }
 #pragma unroll
       for (int q = 0; q < NPT; q += 4) {
@@ -1659,8 +1691,8 @@ fdcn_march(KArgs A) {
         if (q + 4 < NPT) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            tpn[u] = ztab[tb + (q + 4 + u) / S];
-            tgn[u] = ztab[tb + M + (q + 4 + u) / S];
+            tpn[u] = lds_ld(tp_ta, (q + 4 + u) / S);
+            tgn[u] = lds_ld(tp_ta, M + (q + 4 + u) / S);
           }
         }
 #pragma unroll
@@ -1671,7 +1703,7 @@ fdcn_march(KArgs A) {
         // the Ikonen-Toivanen update (W, V', Q'; see the re-run form below)
         double pk[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) pk[u] = phit[poff + FDCN_TP_K(u) * L];
+        for (int u = 0; u < 4; ++u) pk[u] = lds_ld(tp_pa, FDCN_TP_K(u) * L);
         asm volatile(
             "v_fma_f64 %4, %12, %0, -%4\n\t"
             "v_fma_f64 %5, %12, %1, -%5\n\t"
@@ -1738,7 +1770,8 @@ fdcn_march(KArgs A) {
       }
       g = smc_l * y0;
       // lane-major rows, stride NPT+1: bank-spread, immediate offsets
-      zoff = opaque(zoff_cur);
+      if constexpr (kZLds) z_a = hide_addr(z_a);
+      else zoff = opaque(zoff_cur);
     }
     if constexpr (kSplit) {
       // x = s (T + g z) - c2 V: c2 = 1 for theta = 1/2; the Rannacher steps
@@ -1772,7 +1805,7 @@ fdcn_march(KArgs A) {
       double zn[4], pn[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        zn[i] = do_sm ? ztab[zoff + i] : 0.0;
+        zn[i] = do_sm ? (kZLds ? lds_ld(z_a, i) : ztab[zoff + i]) : 0.0;
         if constexpr (IT) pn[i] = phi_at(i);
       }
 #pragma unroll
@@ -1786,7 +1819,7 @@ fdcn_march(KArgs A) {
         if (k + 4 < NPT) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            zn[i] = do_sm ? ztab[zoff + k + 4 + i] : 0.0;
+            zn[i] = do_sm ? (kZLds ? lds_ld(z_a, k + 4 + i) : ztab[zoff + k + 4 + i]) : 0.0;
             if constexpr (IT) pn[i] = phi_at(k + 4 + i);
           }
         }
