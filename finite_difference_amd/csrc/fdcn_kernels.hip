@@ -927,9 +927,14 @@ fdcn_march(KArgs A) {
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
       if constexpr (W == 1) {
-        // stages 0-1 unconditionally (a stage below the 1e-18 cut only adds
-        // a negligible term), the rest behind one uniform branch
-        if (j < 2) b = fma(FW[j], scan_up(b, d, lane4), b);
+        // stages 0-1 inline, the rest behind one uniform branch.  The split
+        // form tests stages 0-1 too (config 3 scenarios need one or two:
+        // 5.17 -> 5.12 ms in A/B).  IT and the recovery form run them
+        // unconditionally: configs 2 and 5 need none (|fm|^(NPT-1) < 1e-18,
+        // the neighbour's aggregate is the whole carry), yet skipping them
+        // measured no faster there (11.03 / 17.52 -> 11.03 / 17.65 ms), the
+        // branches splitting the dependent chain the scheduler overlaps
+        if (j < 2 && (!kSplit || j < nst_f)) b = fma(FW[j], scan_up(b, d, lane4), b);
       } else if (j < nst_f) {
         b = fma(FW[j], scan_up(b, d, lane4), b);
       }
@@ -995,7 +1000,7 @@ fdcn_march(KArgs A) {
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
       if constexpr (W == 1) {
-        if (j < 2) cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
+        if (j < 2 && (!kSplit || j < nst_b)) cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
       } else if (j < nst_b) {
         cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
       }
