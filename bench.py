@@ -81,6 +81,8 @@ DEFAULT_BATCH = {"american": 4096, "barrier": 10000, "double": 2048, "analytic":
 TRADE_WORKLOADS = ("trade_cnlog", "trade_american", "trade_double", "scenario_file",
                    "american_file")
 KERNEL_SRC = os.path.join(ROOT, "finite_difference_amd", "csrc", "fdcn_kernels.hip")
+# GPU vs oracle bound of the parity record (tests/test_gpu_kernels.py TOL)
+PARITY_TOL = 1e-10
 
 
 def parse(argv=None):
@@ -91,6 +93,14 @@ def parse(argv=None):
     ap.add_argument("--workload", choices=sorted(DEFAULT_BATCH) + list(TRADE_WORKLOADS),
                     default="american")
     ap.add_argument("--batch", type=int, default=0, help="scenarios per GPU (0: workload default)")
+    ap.add_argument("--total", type=int, default=0,
+                    help="strong scaling (BASELINE config 4): ONE batch of this many scenarios, "
+                         "built identically on every rank; rank r marches its contiguous "
+                         "shard (distributed.shard_range)")
+    ap.add_argument("--lib", default="", help="A/B timing: load this build of libfdcn.so")
+    ap.add_argument("--force-variant", default="",
+                    help="A/B timing: W,NPT[,FLAVOUR] pinned through fdcn_force_variant "
+                         "(include/fdcn_diag.h)")
     ap.add_argument("--n-space", type=int, default=0, help="0: workload default")
     ap.add_argument("--n-time", type=int, default=0, help="0: workload default")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -104,8 +114,9 @@ def parse(argv=None):
 # ---------------------------------------------------------------------------
 # workloads
 # ---------------------------------------------------------------------------
-def build_american(B: int, n_space: int, n_time: int, seed: int):
-    """B American puts of the notebook trade over a strike x vol sweep."""
+def build_american(B: int, n_space: int, n_time: int, seed: int, select=None):
+    """B American puts of the notebook trade over a strike x vol sweep
+    (scenarios `select` of them only, default all)."""
     from finite_difference_amd import market
     from finite_difference_amd.american import AmericanFDMPricer
     from finite_difference_amd.engine import pack
@@ -113,7 +124,7 @@ def build_american(B: int, n_space: int, n_time: int, seed: int):
     curve = market.iso_curve(market.create_rate_df(math.exp(0.07053828272) - 1.0))
     solves = []
     p = None  # one pricer, re-pointed per scenario (same dates and curve)
-    for i in range(B):
+    for i in (range(B) if select is None else select):
         j = (i * 2654435761 + seed * 97) % B  # deterministic shuffle
         strike = 140.0 + 70.0 * (j % 64) / 63.0
         sigma = 0.18 + 0.30 * ((j // 64) % 64) / 63.0
@@ -126,10 +137,10 @@ def build_american(B: int, n_space: int, n_time: int, seed: int):
         p._reset_trade(176.39, strike, sigma)
         p._build_log_grid()
         solves.append(p._segment_solve(p._payoff_array(), 0.0, p.time_to_expiry, n_time, True))
-    return pack(solves, list(range(B)))
+    return pack(solves, list(range(len(solves))))
 
 
-def build_barrier(B: int, n_space: int, n_time: int, seed: int):
+def build_barrier(B: int, n_space: int, n_time: int, seed: int, select=None):
     """the config_scenarios.csv trade swept over strike,
     vol and barrier; types cycle up/down-out/in x call/put; explicit grid.  A
     knock-in's march is its knock-out twin's (in/out parity), so every
@@ -144,11 +155,14 @@ def build_barrier(B: int, n_space: int, n_time: int, seed: int):
     solves = []
     S0 = 229.74
     calc = {}  # one pricer per option type, re-pointed per scenario (scenarios.run_rows_batched)
-    for i in range(B):
+    sel = range(B) if select is None else select
+    for i in range(B):  # the draws of every scenario, so a shard sees the same batch
         bt = kinds[i % 4]
         K, sig = float(rng.uniform(150, 300)), float(rng.uniform(0.15, 0.45))
         up = float(rng.uniform(1.02, 1.5) * S0) if "up" in bt else None
         lo = float(rng.uniform(0.6, 0.98) * S0) if "down" in bt else None
+        if i not in sel:
+            continue
         opt = ("call", "put")[(i // 4) % 2]
         p = calc.get(opt)
         if p is None:
@@ -159,19 +173,19 @@ def build_barrier(B: int, n_space: int, n_time: int, seed: int):
         p._reset_trade(S0, K, sig, bt, lo, up)
         p.barrier_type = p._map_KI_to_KO() or p.barrier_type
         solves.append(p._make_solve(True, p.sigma)[0])
-    grp = pack(solves, list(range(B)))
+    grp = pack(solves, list(range(len(solves))))
     grp.top_dropped = True  # n_nodes = N_s configured nodes (…pricer.py:449, :543)
     return grp
 
 
-def build_double(B: int, n_space: int, n_time: int, seed: int):
+def build_double(B: int, n_space: int, n_time: int, seed: int, select=None):
     """BASELINE config 5: double knock-out call of double _barrier.py:139-146,
     knock-out projected every step; B > 1 sweeps sigma and the barriers."""
     from finite_difference_amd.engine import pack
     from finite_difference_amd.fd_barrier import FDDoubleBarrier
     b, r, T = 0.049493018, 0.0709454892, 49 / 365
     solves = []
-    for i in range(B):
+    for i in (range(B) if select is None else select):
         j = (i * 2654435761 + seed * 97) % max(B, 1)
         f = j / max(B - 1, 1)
         sig = 0.10994120968 * (0.8 + 0.4 * f) if B > 1 else 0.10994120968
@@ -180,7 +194,7 @@ def build_double(B: int, n_space: int, n_time: int, seed: int):
         d = FDDoubleBarrier(20.786, 21.0, lo, hi, sig, "c", "out", n_space=n_space,
                             n_time=n_time)
         solves.append(d.solve_for(b, r, T))
-    return pack(solves, list(range(B)))
+    return pack(solves, list(range(len(solves))))
 
 
 WORKLOADS = {  # name -> (builder, n_space, n_time, IT?, config label)
@@ -232,36 +246,58 @@ def _cpu_model() -> str:
         return platform.processor()
 
 
-def cpu_baseline(group, seconds: float):
+def host_cores():
+    """(threads to use, record) for the CPU baseline: every core of the
+    process's affinity set, capped by the cgroup CPU quota when one is set
+    (a GPU box grants one-GPU jobs a share of its CPUs; threads beyond the
+    quota only time-slice).  The record lists all three numbers."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) / float(period)))
+    except Exception:
+        pass
+    n = min(affinity, quota) if quota else affinity
+    return n, {"affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+               "omp_max_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(group, seconds: float, res=None):
     """Two variants of the reference algorithm, each on a
     bounded sample of the same batch:
       (i)  C oracle: sequential Thomas (+ IT / KO) per scenario, the
-           reference's loops, OpenMP over scenarios on the host cores the
-           process may use;
+           reference's loops, OpenMP over scenarios on every host core the
+           process may use (host_cores);
       (ii) NumPy batched over scenarios: the same loops with every per-node
            operation vectorised across scenarios (one core).
-    The line's value is the faster one; both are listed."""
+    The line's value is the faster one; both are listed.  The C oracle's
+    outputs are the parity check of the GPU outputs `res` of the same
+    scenarios (whole grid, every node): the "parity" record."""
     import numpy as np
     from oracle import batched_numpy, oracle
-    affinity = len(os.sched_getaffinity(0))
-    nthreads = min(oracle.max_threads(), affinity,
-                   int(os.environ.get("OMP_NUM_THREADS", affinity)))
+    nthreads, cores_rec = host_cores()
     model = _cpu_model()
     # (i) C oracle over whole scenarios, doubling the sample until `seconds`
     done, t_total, m = 0, 0.0, nthreads
+    ref_parts = []
     while t_total < seconds and done < group.B:
         m = min(m, group.B - done)
         sl = slice(done, done + m)
         t0 = time.perf_counter()
         if group.it:
-            oracle.it_batch(group.n_nodes, group.n_time, group.n_ranna, group.params[sl],
-                            group.iparams[sl], group.v_init[sl], group.payoff[sl], nthreads)
+            out = oracle.it_batch(group.n_nodes, group.n_time, group.n_ranna, group.params[sl],
+                                  group.iparams[sl], group.v_init[sl], group.payoff[sl],
+                                  nthreads)
         else:
             # monitor runs are addressed by MON_START/MON_COUNT: pass the full arrays
-            oracle.cn_batch(group.n_nodes, group.n_time, group.n_ranna, group.params[sl],
-                            group.iparams[sl], group.v_init[sl], group.mon_step,
-                            group.mon_rebate, nthreads)
+            out = oracle.cn_batch(group.n_nodes, group.n_time, group.n_ranna, group.params[sl],
+                                  group.iparams[sl], group.v_init[sl], group.mon_step,
+                                  group.mon_rebate, nthreads)
         t_total += time.perf_counter() - t0
+        ref_parts.append(out)
         done += m
         m *= 2
     c_rate = done * node_units(group) * group.n_time / t_total
@@ -269,6 +305,19 @@ def cpu_baseline(group, seconds: float):
              "variant": "C oracle, per-scenario Thomas, OpenMP over scenarios",
              "sample": f"{done} of the {group.B} scenarios, full {node_units(group)}x"
                        f"{group.n_time} grid, {t_total:.1f} s"}
+    parity = None
+    if res is not None:
+        ref = np.concatenate(ref_parts)
+        got = res[:done]
+        scale = np.maximum(1.0, np.max(np.abs(ref), axis=1))
+        rel = np.max(np.abs(got - ref), axis=1) / scale
+        parity = {"max_rel_err": float(np.max(rel)) if rel.size else None,
+                  "n_compared": int(done), "nodes_per_scenario": int(group.n_nodes),
+                  "tol": PARITY_TOL, "ok": bool(np.all(rel <= PARITY_TOL)),
+                  "all_finite": bool(np.all(np.isfinite(got))),
+                  "rule": "per scenario max_j |V_gpu - V_oracle| / max(1, max_j |V_oracle|), "
+                          "every node of the timed launch's output vs the C oracle "
+                          "(oracle/fdcn_oracle.c) on the same scenarios"}
     # (ii) NumPy batched over up to 4096 scenarios, a prefix of the time steps
     nb = min(group.B, 4096)
     kw = dict(payoff=group.payoff[:nb]) if group.it else dict(
@@ -289,13 +338,14 @@ def cpu_baseline(group, seconds: float):
               "sample": f"{nb} scenarios x first {steps} of {group.n_time} steps, full "
                         f"{node_units(group)}-node grid, {t_np:.1f} s"}
     best = c_var if c_rate >= np_rate else np_var
-    return {"value": best["value"], "unit": "node-steps/s", "cores": best["cores"],
-            "kind": "port",
-            "sample": best["sample"] + f"; {best['variant']} ("
-                      + ("fd_american_equity.py:559-726" if group.it else
-                         "discrete_barrier_fdm_pricer.py:442-547")
-                      + f") on {model}",
-            "affinity_cpus": affinity, "variants": [c_var, np_var]}
+    cpu = {"value": best["value"], "unit": "node-steps/s", "cores": best["cores"],
+           "kind": "port",
+           "sample": best["sample"] + f"; {best['variant']} ("
+                     + ("fd_american_equity.py:559-726" if group.it else
+                        "discrete_barrier_fdm_pricer.py:442-547")
+                     + f") on {model}",
+           **cores_rec, "variants": [c_var, np_var]}
+    return cpu, parity
 
 
 # ---------------------------------------------------------------------------
@@ -313,7 +363,13 @@ def _rank_entry(local_rank: int, argv, port: int, world: int) -> None:
     os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
                       LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
-    run_rank(parse(argv))
+    args = parse(argv)
+    if args.lib:
+        from finite_difference_amd import capi
+        capi.LIB_PATH = os.path.abspath(args.lib)
+    rc = run_rank(args)
+    if rc:
+        raise SystemExit(rc)
 
 
 def spawn_ranks(args, argv) -> int:
@@ -341,24 +397,33 @@ def run_rank(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.dry_run:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.dry_run:
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
         return dry_run_rank(args, world, rank, local)
     from finite_difference_amd import capi, distributed
-    bound = distributed.bind_device()  # GPU LOCAL_RANK for libfdcn and torch
+    bound = distributed.bind_device()  # this rank's GPU for libfdcn and torch
     if bound is None:
         raise capi.FdcnError("no gfx950 device visible; the benchmark needs an MI355X")
-    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", bound))
+    if args.force_variant:
+        capi.force_variant(*[int(x) for x in args.force_variant.split(",")])
+    dev = torch.device("cuda", bound)
     builder, ns0, nt0, is_it, label = WORKLOADS[args.workload]
-    B = args.batch or DEFAULT_BATCH[args.workload]
     n_space, n_time = args.n_space or ns0, args.n_time or nt0
     t_build = time.perf_counter()
-    g = builder(B, n_space, n_time, seed=rank)
+    if args.total:
+        # config 4: one batch of `total` scenarios (the same draws on every
+        # rank), rank r marches its contiguous shard -- strong scaling
+        mine = distributed.shard_range(args.total, rank, world)
+        g = builder(args.total, n_space, n_time, seed=0, select=mine)
+        B = g.B
+    else:
+        B = args.batch or DEFAULT_BATCH[args.workload]
+        g = builder(B, n_space, n_time, seed=rank)
     t_build = time.perf_counter() - t_build
     k_cap = capi.sm_extent(g.n_nodes, g.n_time, g.n_ranna, g.params)
     plan = capi.plan(g.n_nodes, is_it, k_cap, n_time=g.n_time, B=g.B)
@@ -407,30 +472,40 @@ def run_rank(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
+    # whole-job node-steps: every rank's batch (they differ by one scenario
+    # at most under --total), summed over the ranks
+    node_steps_launch = g.B * node_units(g) * g.n_time  # configured nodes x steps x solves
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tot = torch.tensor([float(node_steps_launch)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         elapsed = float(t.item())
+        job_node_steps = float(tot.item())
+    else:
+        job_node_steps = float(node_steps_launch)
 
     res = out.cpu().numpy()
     finite = bool(np.all(np.isfinite(res)))
-    node_steps_launch = g.B * node_units(g) * g.n_time  # configured nodes x steps x solves
-    total = node_steps_launch * args.steps * world
+    total = job_node_steps * args.steps
     value = total / elapsed
-    workload = f"{label}_{n_space}x{n_time}_batch{B}"
+    workload = (f"{label}_{n_space}x{n_time}_total{args.total}" if args.total
+                else f"{label}_{n_space}x{n_time}_batch{B}")
     bps, fps = BYTES_PER_NODE_STEP[is_it], FLOPS_PER_NODE_STEP[is_it]
     kernel_s = kernel_ms * 1e-3
     achieved_tf = fps * node_steps_launch / kernel_s / 1e12
     achieved_gbs = bps * node_steps_launch / kernel_s / 1e9
     ctr = load_counters(workload)
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(g, args.cpu_seconds)
+        cpu, parity = cpu_baseline(g, args.cpu_seconds, res)
 
     if rank == 0:
         config = {"workload": workload, "scenarios_per_gpu": g.B, "grid": [n_space, n_time],
                   "parallelism": f"scenario-sharded x{world}"}
+        if args.total:
+            config.update(total_scenarios=args.total, shard="contiguous (shard_range)")
         if is_it:
             config.update(option="american put", exercise="ikonen-toivanen", rannacher_steps=2)
         elif args.workload == "barrier":
@@ -442,10 +517,12 @@ def run_rank(args):
         valu = None
         if ctr and ctr.get("valu_insts_per_launch"):
             insts = float(ctr["valu_insts_per_launch"])
-            valu = {"valu_insts_per_node_step": insts / node_steps_launch,
+            valu = {"valu_insts_per_lane_node_step": 64 * insts / node_steps_launch,
                     "issue_frac": insts * 4 / (N_SIMD * VALU_CLOCK_GHZ * 1e9 * kernel_s),
-                    "note": "SQ_INSTS_VALU of this kernel source (profiles/pmc_counters.json) "
-                            "x 4 clk per wave64 fp64 op / (1024 SIMDs x 2.4 GHz x launch time)"}
+                    "note": "SQ_INSTS_VALU (wave instructions) of this kernel source "
+                            "(profiles/pmc_counters.json) x 64 lanes / node-steps; issue: x 4 clk "
+                            "per wave64 fp64 op / (1024 SIMDs x 2.4 GHz x launch time)"}
+        fv = capi.forced_variant()
         line = {
             "metric": "CN grid-node-steps/sec/GPU (2048x4096 grid); achieved HBM GB/s vs peak",
             "value": value,
@@ -455,7 +532,7 @@ def run_rank(args):
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.total else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (" + {"american": "strike x vol sweep of the notebook American put",
@@ -479,14 +556,21 @@ def run_rank(args):
             "value_per_gpu": value / world,
             "kernel_ms_per_launch": kernel_ms,
             "kernel": {"name": f"fdcn_march<IT={int(is_it)}>", **plan, "k_cap": k_cap,
-                       "src_sha": kernel_src_sha()},
+                       "src_sha": kernel_src_sha(),
+                       "forced": list(fv) if fv[0] else None,
+                       "lib": capi.LIB_PATH if args.lib else None},
             "outputs_finite": finite,
+            "parity": parity,
             "host_build_s": t_build,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if parity is not None and not (parity["ok"] and parity["all_finite"]):
+        print(f"bench.py: PARITY FAILURE {parity}", file=sys.stderr, flush=True)
+        return 3
+    return 0
 
 
 def dry_run_rank(args, world: int, rank: int, local: int):
@@ -501,6 +585,10 @@ def dry_run_rank(args, world: int, rank: int, local: int):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ranks = [{"rank": rank, "local_rank": local, "pid": os.getpid()}]
+    if args.total:  # the shard this rank would march (config 4)
+        from finite_difference_amd.distributed import shard_range
+        r = shard_range(args.total, rank, world)
+        ranks[0]["shard"] = [r.start, r.stop]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -715,8 +803,7 @@ def bench_analytic(args):
     from finite_difference_amd import capi, distributed
     from finite_difference_amd.analytic import BarrierEngine
     capi.require_device()
-    distributed.bind_device()
-    dev = torch.device("cuda", distributed.local_rank())
+    dev = torch.device("cuda", distributed.bind_device())
     B = args.batch or DEFAULT_BATCH["analytic"]
     rng = np.random.default_rng(20250728)
     s = rng.uniform(50, 150, B)
@@ -789,6 +876,9 @@ def bench_analytic(args):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    if args.lib:
+        from finite_difference_amd import capi
+        capi.LIB_PATH = os.path.abspath(args.lib)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         if args.workload in TRADE_WORKLOADS or args.workload == "analytic":
             raise SystemExit(f"--workload {args.workload} is a single-GPU measurement")

@@ -16,11 +16,12 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(HERE, "_lib")
-# FDCN_LIB points at an alternative build of the same library (A/B timing of
-# kernel variants only; unset in every test, smoke and bench run)
-LIB_PATH = os.environ.get("FDCN_LIB") or os.path.join(LIB_DIR, "libfdcn.so")
+# the in-tree build; bench.py --lib points it at an A/B build before the
+# first load (timing of kernel variants only)
+LIB_PATH = os.path.join(LIB_DIR, "libfdcn.so")
 REPO_ROOT = os.path.dirname(HERE)
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "fdcn.h")
+DIAG_HEADER_PATH = os.path.join(REPO_ROOT, "include", "fdcn_diag.h")
 
 # mirrors of the enums in include/fdcn.h
 P_DT, P_A, P_C, P_BC, P_TAU0 = 0, 1, 2, 3, 4
@@ -41,7 +42,10 @@ EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batc
             "fdcn_session_destroy", "fdcn_session_slots", "fdcn_session_march",
             "fdcn_session_dividend_jump", "fdcn_session_greeks", "fdcn_session_fetch",
             "fdcn_vc_batch", "fdcn_vc_batch_dev", "fdcn_vc_plan", "fdcn_barrier_plan",
-            "fdcn_vmath", "fdcn_american_plan")
+            "fdcn_vmath", "fdcn_american_plan", "fdcn_device_ordinals")
+# include/fdcn_diag.h: test / tuning entry points, not the product boundary
+DIAG_EXPORTED = ("fdcn_force_variant", "fdcn_forced_variant", "fdcn_variant_name")
+FLAVOUR_THROUGHPUT, FLAVOUR_LATENCY, FLAVOUR_PAIRED = 0, 1, 2
 VC_NDIAG = 6
 RR_NPARAM, RR_NFLAG = 8, 5
 DB_NPARAM, DB_NFLAG = 8, 3
@@ -61,6 +65,59 @@ _V = ctypes.c_void_p
 _I64 = ctypes.c_int64
 
 
+def elf_dynamic_names(path: str) -> dict:
+    """{"soname": str | None, "needed": [str]} from an ELF64 shared object's
+    dynamic section (read from the file; nothing is loaded)."""
+    import struct
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        raise ValueError(f"{path}: not an ELF64 object")
+    e_phoff, = struct.unpack_from("<Q", data, 0x20)
+    e_phentsize, e_phnum = struct.unpack_from("<HH", data, 0x36)
+    loads, dyn = [], None
+    for i in range(e_phnum):
+        p_type, _, p_offset, p_vaddr, _, p_filesz = struct.unpack_from(
+            "<IIQQQQ", data, e_phoff + i * e_phentsize)
+        if p_type == 1:
+            loads.append((p_vaddr, p_offset, p_filesz))
+        elif p_type == 2:
+            dyn = (p_offset, p_filesz)
+    if dyn is None:
+        return {"soname": None, "needed": []}
+
+    def file_off(vaddr):
+        for va, off, sz in loads:
+            if va <= vaddr < va + sz:
+                return off + vaddr - va
+        raise ValueError("address outside the loaded segments")
+    entries, strtab = [], None
+    for k in range(dyn[1] // 16):
+        tag, val = struct.unpack_from("<qQ", data, dyn[0] + 16 * k)
+        if tag == 0:
+            break
+        if tag == 5:  # DT_STRTAB
+            strtab = file_off(val)
+        entries.append((tag, val))
+
+    def cstr(o):
+        return data[strtab + o:data.index(b"\0", strtab + o)].decode()
+    return {"soname": next((cstr(v) for t, v in entries if t == 14), None),  # DT_SONAME
+            "needed": [cstr(v) for t, v in entries if t == 1]}              # DT_NEEDED
+
+
+def _torch_hip_runtime() -> Optional[str]:
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except Exception:
+        return None
+    if spec is None or not spec.origin:
+        return None
+    path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    return path if os.path.exists(path) else None
+
+
 def _preload_hip_runtime() -> None:
     """Load the HIP runtime PyTorch ships (torch/lib/libamdhip64.so) before
     libfdcn, so a process that uses both -- device tensors for the _dev entry
@@ -68,16 +125,18 @@ def _preload_hip_runtime() -> None:
     dependency (soname libamdhip64.so.7) then binds to the copy already
     loaded; loading libfdcn first would map /opt/rocm's copy and torch would
     later add a second one (its NEEDED entry is the unversioned name).
-    torch is not imported; without it /opt/rocm's runtime is used."""
-    import importlib.util
+    Only when torch's copy carries the SONAME libfdcn needs: another major
+    version would not satisfy libfdcn's dependency, and preloading it would
+    itself make two runtimes.  torch is not imported."""
+    path = _torch_hip_runtime()
+    if path is None:
+        return
     try:
-        spec = importlib.util.find_spec("torch")
-    except Exception:
+        want = [n for n in elf_dynamic_names(LIB_PATH)["needed"] if n.startswith("libamdhip64")]
+        have = elf_dynamic_names(path)["soname"]
+    except (OSError, ValueError):
         return
-    if spec is None or not spec.origin:
-        return
-    path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
-    if os.path.exists(path):
+    if want and have == want[0]:
         ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 
 
@@ -122,6 +181,8 @@ def lib() -> ctypes.CDLL:
             L.fdcn_last_error.argtypes = []
             L.fdcn_device_count.restype = ctypes.c_int
             L.fdcn_device_count.argtypes = []
+            L.fdcn_device_ordinals.restype = ctypes.c_int
+            L.fdcn_device_ordinals.argtypes = [_PI, _I]
             L.fdcn_abi_version.restype = ctypes.c_int
             L.fdcn_abi_version.argtypes = []
             L.fdcn_tau_sequence.restype = _I
@@ -148,6 +209,12 @@ def lib() -> ctypes.CDLL:
             L.fdcn_select_device.argtypes = [_I]
             L.fdcn_current_device.restype = ctypes.c_int
             L.fdcn_current_device.argtypes = []
+            L.fdcn_force_variant.restype = _I
+            L.fdcn_force_variant.argtypes = [_I, _I, _I]
+            L.fdcn_forced_variant.restype = _I
+            L.fdcn_forced_variant.argtypes = [_PI, _PI, _PI]
+            L.fdcn_variant_name.restype = _I
+            L.fdcn_variant_name.argtypes = [_I, _I, _I, _I, ctypes.c_char_p, _I]
             if L.fdcn_abi_version() != ABI_VERSION:
                 raise FdcnError("libfdcn.so ABI version mismatch; rebuild")
             _lib = L
@@ -171,6 +238,13 @@ def device_count() -> int:
     return _n_devices
 
 
+def device_ordinals() -> list:
+    """HIP ordinals of the visible gfx950 devices (ascending)."""
+    buf = (ctypes.c_int32 * 64)()
+    n = int(lib().fdcn_device_ordinals(buf, 64))
+    return [int(buf[i]) for i in range(min(n, 64))]
+
+
 def require_device() -> None:
     if device_count() < 1:
         raise FdcnError("no gfx950 (MI355X) device visible; the CN engine has no CPU path")
@@ -187,6 +261,27 @@ def current_device() -> int:
     if d < 0:
         _check(d)
     return d
+
+
+def force_variant(waves: int, npt: int = 0, flavour: int = FLAVOUR_THROUGHPUT) -> None:
+    """Diagnostics (include/fdcn_diag.h): pin every later march launch of this
+    process to the compiled variant (waves, npt, flavour) where it fits;
+    waves = 0 clears.  Tests and A/B tools only -- the product never calls it."""
+    _check(lib().fdcn_force_variant(int(waves), int(npt), int(flavour)))
+
+
+def forced_variant() -> tuple:
+    w, n, f = (ctypes.c_int32() for _ in range(3))
+    _check(lib().fdcn_forced_variant(ctypes.byref(w), ctypes.byref(n), ctypes.byref(f)))
+    return w.value, n.value, f.value
+
+
+def variant_name(n_nodes: int, it_mode: bool, k_cap: int = 0, *, B: int) -> str:
+    """The kernel instance ("fdcn_march<IT,W,NPT,ZG>") a launch of B scenarios
+    runs, the override included (diagnostics, include/fdcn_diag.h)."""
+    buf = ctypes.create_string_buffer(64)
+    _check(lib().fdcn_variant_name(int(B), int(n_nodes), 1 if it_mode else 0, int(k_cap), buf, 64))
+    return buf.value.decode()
 
 
 def _f64(a) -> np.ndarray:

@@ -46,11 +46,13 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <type_traits>
 #include <vector>
 
 #include "../../include/fdcn.h"
+#include "../../include/fdcn_diag.h"
 
 namespace {
 
@@ -2077,7 +2079,8 @@ Variant mk() {
 // VGPRs (16 waves on one CU), so they use short chunks.
 #define FDCN_VARIANTS(IT)                                                                   \
   mk<IT, 1, 4>(), mk<IT, 1, 8>(), mk<IT, 1, 12>(), mk<IT, 1, 16>(), mk<IT, 1, 24>(),        \
-      mk<IT, 1, 32>(), mk<IT, 1, 40>(), mk<IT, 1, 48>(), mk<IT, 1, 64>(), mk<IT, 2, 16>(),  \
+      mk<IT, 1, 32>(), mk<IT, 1, 40>(), mk<IT, 1, 48>(), mk<IT, 1, 64>(), mk<IT, 2, 8>(),   \
+      mk<IT, 2, 16>(),                                                                      \
       mk<IT, 2, 32>(), mk<IT, 2, 40>(), mk<IT, 4, 8>(), mk<IT, 4, 16>(), mk<IT, 4, 24>(),   \
       mk<IT, 4, 40>(), mk<IT, 8, 8>(), mk<IT, 8, 16>(), mk<IT, 8, 40>(), mk<IT, 16, 8>(),   \
       mk<IT, 16, 24>(), mk<IT, 16, 40>(), mk<IT, 1, 64, 1>(), mk<IT, 4, 40, 1>(),           \
@@ -2123,26 +2126,34 @@ bool fits(const Variant& v, int n_int, int k_cap, bool no_idle_wave = true) {
 // Waves the chip keeps resident at the design occupancy (256 CUs x 8).
 constexpr long kResidentWaves = 2048;
 
+// Diagnostics override (include/fdcn_diag.h): (waves, npt, flavour) packed
+// as w | npt << 8 | flavour << 16, 0 = none.  Set only by
+// fdcn_force_variant -- the launch path never reads the environment.
+std::atomic<int> g_forced{0};
+
+const Variant* forced_variant(int n_int, int it, int k_cap) {
+  const int f = g_forced.load(std::memory_order_relaxed);
+  if (!f) return nullptr;
+  const int w = f & 0xff, npt = (f >> 8) & 0xff, fl = f >> 16;
+  for (int zg = 0; zg < 2; ++zg)
+    for (int i = 0; i < kNumVariants; ++i) {
+      const Variant& v = kVariants[i];
+      if (v.it == it && v.w == w && v.npt == npt && v.zg == zg && v.lat == (fl == 1) &&
+          v.pair == (fl == 2) && fits(v, n_int, k_cap, zg == 0))
+        return &v;
+    }
+  return nullptr;
+}
+
 // Variant choice.  Large batches (the throughput case): fewest waves per
 // scenario, then the least padding.  Batches too small to fill the chip
 // (B * W_min < kResidentWaves / 2) whose chunks are long (NPT >= 48): spread
 // each scenario over more waves, down to 16-node chunks, while the batch
-// still fits in one residency round.  FDCN_VARIANT="W,NPT" forces a variant
-// (tuning/diagnostics only).
+// still fits in one residency round.
 const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
   const int n_int = n_nodes - 2;
   if (n_int < 3) return nullptr;
-  if (const char* f = getenv("FDCN_VARIANT")) {
-    // "W,NPT" or "W,NPT,F": F=1 single-trade flavour, F=2 paired flavour
-    int w = 0, npt = 0, fl = 0;
-    if (sscanf(f, "%d,%d,%d", &w, &npt, &fl) >= 2)
-      for (int zg = 0; zg < 2; ++zg)
-        for (int i = 0; i < kNumVariants; ++i)
-          if (kVariants[i].it == it && kVariants[i].w == w && kVariants[i].npt == npt &&
-              kVariants[i].zg == zg && kVariants[i].lat == (fl == 1) &&
-              kVariants[i].pair == (fl == 2) && fits(kVariants[i], n_int, k_cap, zg == 0))
-            return &kVariants[i];
-  }
+  if (const Variant* f = forced_variant(n_int, it, k_cap)) return f;
   const Variant* best = nullptr;
   long best_slots = 0;
   int best_w = 0;
@@ -2612,6 +2623,20 @@ int fdcn_device_count(void) {
   return good;
 }
 
+int fdcn_device_ordinals(int32_t* ord, int32_t cap) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  int good = 0;
+  for (int i = 0; i < n; ++i) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) {
+      if (ord && good < cap) ord[good] = i;
+      ++good;
+    }
+  }
+  return good;
+}
+
 int fdcn_abi_version(void) { return FDCN_ABI_VERSION; }
 
 int fdcn_select_device(int32_t ordinal) {
@@ -2627,6 +2652,42 @@ int fdcn_current_device(void) {
   int d = -1;
   if (hipGetDevice(&d) != hipSuccess) return fail(FDCN_EHIP, "hipGetDevice failed");
   return d;
+}
+
+int fdcn_force_variant(int32_t waves, int32_t npt, int32_t flavour) {
+  if (waves == 0) {
+    g_forced.store(0);
+    return FDCN_OK;
+  }
+  if (flavour < FDCN_FLAVOUR_THROUGHPUT || flavour > FDCN_FLAVOUR_PAIRED)
+    return fail(FDCN_EINVAL, "fdcn_force_variant: flavour %d outside [0, 2]", flavour);
+  for (int i = 0; i < kNumVariants; ++i) {
+    const Variant& v = kVariants[i];
+    if (v.w == waves && v.npt == npt && v.lat == (flavour == 1) && v.pair == (flavour == 2)) {
+      g_forced.store(waves | (npt << 8) | (flavour << 16));
+      return FDCN_OK;
+    }
+  }
+  return fail(FDCN_EINVAL, "fdcn_force_variant: no compiled variant W=%d NPT=%d flavour=%d",
+              waves, npt, flavour);
+}
+
+int fdcn_variant_name(int32_t B, int32_t n_nodes, int32_t it_mode, int32_t k_cap, char* buf,
+                      int32_t len) {
+  if (!buf || len < 1) return fail(FDCN_EINVAL, "fdcn_variant_name: buf");
+  const Variant* v = choose(n_nodes, it_mode ? 1 : 0, k_cap, B > 0 ? B : 1);
+  if (!v) return fail(FDCN_EINVAL, "unsupported n_nodes=%d", n_nodes);
+  snprintf(buf, (size_t)len, "fdcn_march<%d,%d,%d,%d>", v->it, v->w, v->npt,
+           v->zg | (v->lat << 1) | (v->pair << 2));
+  return FDCN_OK;
+}
+
+int fdcn_forced_variant(int32_t* waves, int32_t* npt, int32_t* flavour) {
+  const int f = g_forced.load();
+  if (waves) *waves = f & 0xff;
+  if (npt) *npt = (f >> 8) & 0xff;
+  if (flavour) *flavour = f >> 16;
+  return FDCN_OK;
 }
 
 

@@ -361,7 +361,18 @@ struct PinnedArena {
     return r;
   }
   void reset() { cur = used = 0; }
+  // Unpin the chunks beyond the first `keep` bytes (after reset: nothing in
+  // use).  A whole-file plan stages hundreds of MB; an idle context keeps
+  // only what a typical trade needs, not the largest file ever staged.
+  void trim(size_t keep) {
+    size_t held = 0, k = 0;
+    while (k < chunks.size() && held + chunks[k].cap <= keep) held += chunks[k++].cap;
+    for (size_t i = k; i < chunks.size(); ++i) (void)hipHostFree(chunks[i].p);
+    chunks.resize(k);
+  }
 };
+// pinned staging an idle per-thread context keeps between sessions
+constexpr size_t kIdlePinnedBytes = size_t(64) << 20;
 
 // Per-thread, per-device resources a session borrows: streams, spare events
 // and the pinned arena.  Creating them costs far more than a small trade's
@@ -512,13 +523,22 @@ int fdcn_session_destroy(fdcn_session* s) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   if (cur != s->device) (void)hipSetDevice(s->device);
-  for (auto& b : s->blocks)
-    if (hipFreeAsync(b.p, b.s) != hipSuccess) rc = sfail(FDCN_EHIP, "hipFreeAsync failed");
+  // Drain every session stream BEFORE the frees: a block allocated on one
+  // stream is read on others (gather_rows of v_init slots, the dividend
+  // jump, the Greeks epilogue wait on its producer's event), so a free
+  // ordered on the allocating stream alone could hand the block to another
+  // allocation while a consumer still reads it.  After the syncs no work of
+  // the session is pending and the stream-ordered frees are safe.
   for (hipStream_t st : s->streams)
     if (hipStreamSynchronize(st) != hipSuccess) rc = sfail(FDCN_EHIP, "stream sync failed");
+  if (rc == FDCN_OK) {
+    for (auto& b : s->blocks)
+      if (hipFreeAsync(b.p, b.s) != hipSuccess) rc = sfail(FDCN_EHIP, "hipFreeAsync failed");
+  }  // after a failure the blocks are leaked rather than freed under running work
   if (rc == FDCN_OK) {  // everything drained: the resources go back to the thread
     for (hipEvent_t e : s->events) s->ctx->spare_events.push_back(e);
     s->ctx->pinned.reset();
+    s->ctx->pinned.trim(kIdlePinnedBytes);
     t_idle_ctx.push_back(s->ctx);
   }  // after a failure they are dropped (leaked) rather than reused
   if (cur != s->device) (void)hipSetDevice(cur);

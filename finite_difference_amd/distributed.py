@@ -42,29 +42,38 @@ def local_rank() -> int:
 
 
 def bind_device() -> Optional[int]:
-    """One process per GPU: make GPU `local_rank()` current for libfdcn (the
+    """One process per GPU: make this rank's GPU current for libfdcn (the
     host-array entry points run on the calling thread's HIP device) and for
-    torch (RCCL collectives need it).  Returns the ordinal, or None on a host
-    with no gfx950 device (CPU tests over gloo).  Raises if the rank has no
-    GPU of its own -- every rank marching on GPU 0 is the failure this guards."""
+    torch (RCCL collectives need it).  Local rank k binds the k-th visible
+    gfx950 device (its HIP ordinal may differ on a host with other GPUs);
+    when exactly one device is visible -- a launcher that hands each rank its
+    own GPU through HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES -- every rank
+    binds that one.  Returns the HIP ordinal, or None on a host with no
+    gfx950 device (CPU tests over gloo).  Raises if several devices are
+    visible but fewer than the local rank needs: every rank marching on GPU 0
+    is the failure this guards."""
     from . import capi
     try:
-        n = capi.device_count()
+        ords = capi.device_ordinals()
     except capi.FdcnError:
         return None
-    if n == 0:
+    if not ords:
         return None
     lr = local_rank()
-    if lr >= n:
-        raise capi.FdcnError(f"LOCAL_RANK={lr} but only {n} gfx950 device(s) are visible")
-    capi.select_device(lr)
+    if len(ords) == 1:
+        dev = ords[0]
+    elif lr < len(ords):
+        dev = ords[lr]
+    else:
+        raise capi.FdcnError(f"LOCAL_RANK={lr} but only {len(ords)} gfx950 device(s) are visible")
+    capi.select_device(dev)
     try:
         import torch
         if torch.cuda.is_available():
-            torch.cuda.set_device(lr)
+            torch.cuda.set_device(dev)
     except ImportError:  # pragma: no cover - torch is always present here
         pass
-    return lr
+    return dev
 
 
 def shard_range(n: int, rank: Optional[int] = None, world: Optional[int] = None) -> range:
@@ -96,6 +105,32 @@ def gather_rows(rows: List[dict]) -> Optional[List[dict]]:
     for part in out:
         merged.extend(part)
     return merged
+
+
+def gather_columns(cols: dict) -> Optional[dict]:
+    """Concatenate every rank's result columns (name -> list or array) on rank
+    0, in rank order; None elsewhere.  One gather_object of the column dict:
+    arrays travel as arrays, not as per-row dicts."""
+    d = _dist()
+    if d is None:
+        return cols
+    import numpy as np
+    rank, world = d.get_rank(), d.get_world_size()
+    parts = [None] * world if rank == 0 else None
+    d.gather_object(cols, parts, dst=0)
+    if rank != 0:
+        return None
+    parts = [p for p in parts if p]  # a rank with no rows sends an empty dict
+    if not parts:
+        return {}
+    out = {}
+    for k in parts[0]:
+        vals = [p[k] for p in parts]
+        if all(isinstance(v, np.ndarray) for v in vals):
+            out[k] = np.concatenate(vals)
+        else:
+            out[k] = [x for v in vals for x in (v.tolist() if isinstance(v, np.ndarray) else v)]
+    return out
 
 
 def broadcast_rows(rows: Optional[List[dict]]) -> List[dict]:

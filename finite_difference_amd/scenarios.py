@@ -220,31 +220,36 @@ def run_all_scenarios(config_csv_path: str, output_csv_path: Optional[str],
                       base_params: Dict[str, Any], engine: Optional[Engine] = None,
                       verbose: bool = True):
     """Read the configuration CSV, price every row, write the results CSV
-    (run_config_scenarios.py:137-195).  Sharded across ranks when
-    torch.distributed is initialised."""
+    (run_config_scenarios.py:137-195).
+
+    One path at every world size: this rank's contiguous block of rows
+    (all of them without torch.distributed) goes through one native plan
+    build, one launch and the device epilogue (scenario_batch.price_columns);
+    with torch.distributed initialised -- world size 1 included -- rank 0
+    then gathers the result columns (the only collective)."""
     import pandas as pd
     from . import distributed
     from . import scenario_batch
     cfg = pd.read_csv(config_csv_path)
-    if distributed.is_initialized():
-        distributed.bind_device()  # this rank's GPU (LOCAL_RANK), before any launch
-    if distributed.rank_world()[1] == 1:
-        # the whole file in one plan build + one launch (scenario_batch.py)
-        cols = {k: cfg[k].tolist() for k in scenario_batch.ROW_KEYS if k in cfg.columns}
-        priced = scenario_batch.price_columns(cols, base_params, engine)
-        if priced is not None:
-            df = pd.DataFrame(scenario_batch.result_columns(cols, priced))
-            res = df.to_dict("records") if verbose else None
-            return _finish_scenarios(df, res, output_csv_path, verbose)
-    rows = [dict(r) for _, r in cfg.iterrows()]
-    mine = distributed.shard(rows)
-    res = scenario_batch.run_rows_vectorized(mine, base_params, engine)
-    if res is None:
-        res = run_rows_batched(mine, base_params, engine)
-    res = distributed.gather_rows(res)
-    if res is None:  # non-zero rank
-        return None
-    return _finish_scenarios(pd.DataFrame(res), res, output_csv_path, verbose)
+    sharded = distributed.is_initialized()
+    if sharded:
+        distributed.bind_device()  # this rank's GPU, before any launch
+    mine = distributed.shard_range(len(cfg))
+    part = cfg.iloc[mine.start:mine.stop]
+    cols = {k: part[k].tolist() for k in scenario_batch.ROW_KEYS if k in part.columns}
+    priced = scenario_batch.price_columns(cols, base_params, engine)
+    if priced is not None:
+        out = scenario_batch.result_columns(cols, priced)
+    else:  # shapes the whole-file plan declines: the per-row facades, batched
+        rows = run_rows_batched([dict(r) for _, r in part.iterrows()], base_params, engine)
+        out = {k: [r[k] for r in rows] for k in (rows[0] if rows else {})}
+    if sharded:
+        out = distributed.gather_columns(out)
+        if out is None:  # non-zero rank
+            return None
+    df = pd.DataFrame(out)
+    res = df.to_dict("records") if verbose else None
+    return _finish_scenarios(df, res, output_csv_path, verbose)
 
 
 def _finish_scenarios(df, res, output_csv_path, verbose):

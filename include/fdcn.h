@@ -397,6 +397,10 @@ int fdcn_vmath(int32_t op, int64_t n, const double* x, double* y);
 
 const char* fdcn_last_error(void);
 int fdcn_device_count(void);   /* gfx950 devices visible; 0 if none          */
+/* The HIP ordinals of the visible gfx950 devices, ascending, into ord[cap];
+ * returns how many there are (may exceed cap), 0 if none.  On a host with
+ * other GPUs too, local rank k binds ord[k], not HIP ordinal k. */
+int fdcn_device_ordinals(int32_t* ord, int32_t cap);
 int fdcn_abi_version(void);    /* FDCN_ABI_VERSION                           */
 /* Make `ordinal` the calling thread's current HIP device (hipSetDevice): the
  * host-pointer entry points run there.  One process per GPU calls it once

@@ -30,3 +30,15 @@ def oracle_lib():
     from oracle import oracle
     oracle.build()
     return oracle
+
+
+@pytest.fixture
+def force_variant():
+    """Pin the march kernel variant (include/fdcn_diag.h) for one test:
+    force_variant(waves, npt, flavour=0); cleared afterwards."""
+    from finite_difference_amd import capi
+
+    def pin(waves, npt, flavour=0):
+        capi.force_variant(waves, npt, flavour)
+    yield pin
+    capi.force_variant(0)

@@ -52,3 +52,39 @@ def test_trade_workloads_refuse_multi_gpu():
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--workload", "trade_cnlog"],
                        cwd=ROOT, capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and "single-GPU" in p.stderr
+
+
+def test_bench_total_shards_one_batch():
+    """--total (config 4, strong scaling): the ranks split ONE batch into
+    contiguous shards that cover it exactly once."""
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dry-run", "--steps", "1",
+                        "--warmup", "0", "--workload", "barrier", "--total", "10001"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = _last_json(p.stdout)
+    _check(line, 2)
+    assert [r["shard"] for r in line["ranks"]] == [[0, 5001], [5001, 10001]]
+
+
+def test_barrier_builder_shard_equals_slice_of_full_batch():
+    """A rank's shard of the config-4 batch is bit-identical to the same rows
+    of the whole batch built in one process (the draws are not per rank)."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    full = bench.build_barrier(40, 64, 30, seed=0)
+    part = bench.build_barrier(40, 64, 30, seed=0, select=range(13, 27))
+    assert np.array_equal(part.params, full.params[13:27])
+    assert np.array_equal(part.v_init, full.v_init[13:27])
+    ip = full.iparams[13:27].copy()
+    ip[:, 4] -= ip[0, 4]  # monitor runs are re-based in the shard
+    assert np.array_equal(part.iparams, ip)
+
+
+def test_cpu_cores_record():
+    sys.path.insert(0, ROOT)
+    import bench
+    n, rec = bench.host_cores()
+    assert 1 <= n <= rec["affinity_cpus"]
+    if rec["cgroup_cpu_quota"]:
+        assert n <= rec["cgroup_cpu_quota"]

@@ -7,20 +7,54 @@ import re
 from finite_difference_amd import capi
 
 
-def _header_symbols():
-    txt = open(capi.HEADER_PATH).read()
+def _header_symbols(path=None):
+    """Functions declared by include/fdcn.h (or `path`); with path="all",
+    every header under include/."""
+    if path == "all":
+        inc = os.path.dirname(capi.HEADER_PATH)
+        return sorted(set().union(*(_header_symbols(os.path.join(inc, f))
+                                    for f in os.listdir(inc) if f.endswith(".h"))))
+    txt = open(path or capi.HEADER_PATH).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(fdcn_[a-z_]+)\s*\(", txt)))
 
 
 def test_header_matches_binding_list():
     assert _header_symbols() == sorted(capi.EXPORTED)
+    assert _header_symbols(capi.DIAG_HEADER_PATH) == sorted(capi.DIAG_EXPORTED)
+    assert _header_symbols("all") == sorted(capi.EXPORTED + capi.DIAG_EXPORTED)
+
+
+def test_launch_path_reads_no_environment():
+    """The variant choice depends on the arguments and the explicit
+    diagnostics override only: no getenv in libfdcn."""
+    csrc = os.path.join(os.path.dirname(capi.__file__), "csrc")
+    for f in os.listdir(csrc):
+        assert "getenv" not in open(os.path.join(csrc, f)).read(), f
+
+
+def test_force_variant_pins_and_clears():
+    big = capi.variant_name(1024, False, B=10000)
+    assert big == "fdcn_march<0,1,16,0>", big
+    assert capi.variant_name(1024, False, B=8) == "fdcn_march<0,1,16,2>"  # single-trade flavour
+    try:
+        capi.force_variant(1, 16)
+        assert capi.forced_variant() == (1, 16, 0)
+        assert capi.variant_name(1024, False, B=8) == big
+        assert capi.plan(1024, False, B=8)["npt"] == 16
+        with pytest.raises(capi.FdcnError):
+            capi.force_variant(3, 16)  # not compiled
+        assert capi.forced_variant() == (1, 16, 0)  # unchanged by the failed call
+    finally:
+        capi.force_variant(0)
+    assert capi.forced_variant() == (0, 0, 0)
+    assert capi.variant_name(1024, False, B=8) == "fdcn_march<0,1,16,2>"
 
 
 def test_library_exports_all_symbols():
     assert os.path.exists(capi.LIB_PATH), "run __graft_entry__.build() first"
     L = ctypes.CDLL(capi.LIB_PATH)
-    for name in _header_symbols():
+    for name in _header_symbols("all"):
         assert hasattr(L, name), name
 
 

@@ -67,3 +67,28 @@ def test_two_rank_gloo_matches_single_process(tmp_path):
     assert list(got["scenario_name"]) == list(ref["scenario_name"])
     for col in ("model_price", "model_delta", "model_gamma", "model_vega"):
         assert (got[col].to_numpy() == ref[col].to_numpy()).all(), col
+
+
+def test_bind_device_maps_local_rank_through_gfx950_ordinals(monkeypatch):
+    """local rank k binds the k-th visible gfx950 device; a rank
+    that sees exactly one device (HIP_VISIBLE_DEVICES per rank) binds it
+    whatever its LOCAL_RANK; too few devices for the rank is an error."""
+    from finite_difference_amd import capi
+    chosen = []
+    monkeypatch.setattr(capi, "select_device", lambda d: chosen.append(d))
+    monkeypatch.setattr(capi, "device_ordinals", lambda: [0])
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    assert fdist.bind_device() == 0 and chosen[-1] == 0
+    monkeypatch.setattr(capi, "device_ordinals", lambda: [1, 3, 4])
+    assert fdist.bind_device() == 3 and chosen[-1] == 3
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    with pytest.raises(capi.FdcnError):
+        fdist.bind_device()
+    monkeypatch.setattr(capi, "device_ordinals", lambda: [])
+    assert fdist.bind_device() is None
+
+
+def test_gather_columns_without_a_group_is_identity():
+    import numpy as np
+    cols = {"a": [1, 2], "b": np.arange(2.0)}
+    assert fdist.gather_columns(cols) is cols

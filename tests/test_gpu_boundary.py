@@ -198,13 +198,22 @@ def test_sharded_runner_binds_the_rank_device(backend):
     s.close()
     os.environ["LOCAL_RANK"] = "0"
     dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    from finite_difference_amd import distributed
+    gathers = []
+    real_gather = distributed.gather_columns
+
+    def counting_gather(cols):  # the shard -> gather branch runs over this group
+        gathers.append(len(cols["model_price"]))
+        return real_gather(cols)
+    distributed.gather_columns = counting_gather
     try:
-        from finite_difference_amd import distributed
-        assert distributed.bind_device() == 0
-        assert capi.current_device() == 0
+        assert distributed.bind_device() == capi.device_ordinals()[0]
+        assert capi.current_device() == capi.device_ordinals()[0]
         ranked = scenarios.run_all_scenarios(cfg, None, base, verbose=False)
     finally:
+        distributed.gather_columns = real_gather
         dist.destroy_process_group()
         os.environ.pop("LOCAL_RANK", None)
+    assert gathers == [len(plain)], gathers
     for col in ("model_price", "model_delta", "model_gamma", "model_vega"):
         assert np.array_equal(ranked[col].to_numpy(), plain[col].to_numpy()), col

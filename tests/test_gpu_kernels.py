@@ -24,9 +24,9 @@ class OracleBackend:
         from oracle import oracle
         if g.it:
             return oracle.it_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams,
-                                   g.v_init, g.payoff)
+                                   g.v_init, g.payoff, 8)
         return oracle.cn_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams, g.v_init,
-                               g.mon_step, g.mon_rebate)
+                               g.mon_step, g.mon_rebate, 8)
 
 
 def _compare(solves, label, tol=TOL):
@@ -70,29 +70,39 @@ def test_it_vs_oracle(n_nodes, n_time, n_ranna):
     _compare(solves, f"it n={n_nodes} m={n_time} r={n_ranna} {capi.plan(n_nodes, True, B=B)}")
 
 
-# Every compiled (W, NPT) variant, forced through FDCN_VARIANT on a grid that
-# fills it (64*W*NPT - 3 interior nodes: 3 short lanes, no idle wave).  The
-# default choice depends on the batch size, so small test batches alone would
-# not reach the throughput variants the bench uses.
-VARIANTS = [(1, 4), (1, 8), (1, 12), (1, 16), (1, 24), (1, 32), (1, 40), (1, 48), (1, 64),
-            (2, 16), (2, 32), (2, 40), (4, 8), (4, 16), (4, 24), (4, 40), (8, 8), (8, 16),
-            (8, 40), (16, 8), (16, 24), (16, 40)]
+# Every compiled (W, NPT, flavour) variant, forced (fdcn_force_variant) on a
+# grid that fills it (64*W*NPT - 3 interior nodes: 3 short lanes, no idle
+# wave), over 130 steps: three 64-step blocks of boundary terms, so every
+# block-start load and the block loop's carried state are exercised, with
+# half the solves on accumulated tau (TAU_MODE = 1, the American reference's
+# tau += dt) from a non-zero tau0.  The default choice depends on the batch
+# size, so small test batches alone would not reach the throughput variants
+# the bench uses.
+VARIANTS = [(1, 4, 0), (1, 8, 0), (1, 12, 0), (1, 16, 0), (1, 24, 0), (1, 32, 0), (1, 40, 0),
+            (1, 48, 0), (1, 64, 0), (2, 8, 0), (2, 16, 0), (2, 32, 0), (2, 40, 0), (4, 8, 0), (4, 16, 0),
+            (4, 24, 0), (4, 40, 0), (8, 8, 0), (8, 16, 0), (8, 40, 0), (16, 8, 0), (16, 24, 0),
+            (16, 40, 0), (1, 8, 1), (1, 16, 1), (1, 32, 1)]
+N_TIME_BLOCKS = 130
 
 
 @pytest.mark.parametrize("it", [False, True], ids=["cn", "it"])
-@pytest.mark.parametrize("w,npt", VARIANTS, ids=[f"w{w}n{n}" for w, n in VARIANTS])
-def test_every_variant_vs_oracle(w, npt, it, monkeypatch):
-    monkeypatch.setenv("FDCN_VARIANT", f"{w},{npt}")
+@pytest.mark.parametrize("w,npt,fl", VARIANTS, ids=[f"w{w}n{n}f{f}" for w, n, f in VARIANTS])
+def test_every_variant_vs_oracle(w, npt, fl, it, force_variant):
+    force_variant(w, npt, fl)
     n_nodes = 64 * w * npt - 3 + 2
-    n_time = max(6, min(40, 200000 // n_nodes))
-    plan = capi.plan(n_nodes, it, B=3)
+    n_time = N_TIME_BLOCKS
+    plan = capi.plan(n_nodes, it, B=4)
     assert (plan["waves"], plan["npt"]) == (w, npt), plan
-    rng = np.random.default_rng(3000 + 7 * w + npt + (1 if it else 0))
-    solves = [random_solve(rng, n_nodes, n_time, 2, it=it, drop_top=(i == 1)) for i in range(3)]
+    assert capi.variant_name(n_nodes, it, B=4) == f"fdcn_march<{int(it)},{w},{npt},{2 * fl}>"
+    rng = np.random.default_rng(3000 + 7 * w + npt + 11 * fl + (1 if it else 0))
+    solves = [random_solve(rng, n_nodes, n_time, 2, it=it, drop_top=(i == 1)) for i in range(4)]
+    for i, s in enumerate(solves):
+        s.tau_accumulate = i % 2 == 1
+        s.tau0 = 0.0 if i < 2 else 0.037
     # these grids reach 40k nodes with few steps (dt sigma^2/dx^2 up to ~1e5, |fm|
     # within 1e-3 of 1): rounding in the O(n) recurrences of both solvers then
     # grows with n, so the bound scales with n / 2048 above 2048 nodes
-    _compare(solves, f"{'it' if it else 'cn'} forced W={w} NPT={npt} n={n_nodes} m={n_time}",
+    _compare(solves, f"{'it' if it else 'cn'} forced W={w} NPT={npt} F={fl} n={n_nodes} m={n_time}",
              tol=TOL * max(1.0, n_nodes / 2048))
 
 
@@ -145,11 +155,11 @@ def test_device_visible():
 
 
 @pytest.mark.parametrize("ko_lo", [-1, 30, 1500], ids=["none", "inside_table", "covers_table"])
-def test_rec_form_every_step_knockout_vs_oracle(ko_lo, monkeypatch):
+def test_rec_form_every_step_knockout_vs_oracle(ko_lo, force_variant):
     """Config-5 layout (W=1, NPT=64, recovery form) with a knock-out on every
     step.  When the lower side covers the Sherman-Morrison lanes the kernel
     skips the correction on those steps (the projection overwrites it)."""
-    monkeypatch.setenv("FDCN_VARIANT", "1,64")
+    force_variant(1, 64)
     n_nodes, n_time = 4096, 96
     rng = np.random.default_rng(4096 + ko_lo)
     solves = []
@@ -172,8 +182,8 @@ PAIR_CASES = [(8, 32 * 8 - 1, 5), (8, 32 * 8 + 1, 6), (8, 150, 4), (8, 97, 7), (
 
 @pytest.mark.parametrize("npt,n_nodes,B", PAIR_CASES,
                          ids=[f"n{npt}_{n}_{b}" for npt, n, b in PAIR_CASES])
-def test_paired_variant_vs_oracle(npt, n_nodes, B, monkeypatch):
-    monkeypatch.setenv("FDCN_VARIANT", f"1,{npt},2")
+def test_paired_variant_vs_oracle(npt, n_nodes, B, force_variant):
+    force_variant(1, npt, 2)
     plan = capi.plan(n_nodes, False, B=B)
     assert (plan["waves"], plan["npt"], plan["scen_per_block"]) == (1, npt, 2), plan
     rng = np.random.default_rng(5000 + npt + n_nodes + B)
@@ -185,10 +195,10 @@ def test_paired_variant_vs_oracle(npt, n_nodes, B, monkeypatch):
     _compare(solves, f"cn paired NPT={npt} n={n_nodes} B={B}")
 
 
-def test_paired_every_step_knockout_vs_oracle(monkeypatch):
+def test_paired_every_step_knockout_vs_oracle(force_variant):
     """Knock-out schedules that differ between the two scenarios of a wave:
     every step on one, sparse on the other, rebates on both sides."""
-    monkeypatch.setenv("FDCN_VARIANT", "1,8,2")
+    force_variant(1, 8, 2)
     n_nodes, n_time = 256, 80
     rng = np.random.default_rng(99)
     solves = []

@@ -60,10 +60,10 @@ def test_ko_on_last_step_is_exact(n_nodes, n_time):
         assert not np.all(v[~hit] == s.mon_rebates[-1])
 
 
-@pytest.mark.parametrize("variant", [None, "1,64"], ids=["latency", "rec_form"])
-def test_cn_config5_grid_is_linear(variant, monkeypatch):
+@pytest.mark.parametrize("variant", [None, (1, 64)], ids=["latency", "rec_form"])
+def test_cn_config5_grid_is_linear(variant, force_variant):
     if variant:
-        monkeypatch.setenv("FDCN_VARIANT", variant)
+        force_variant(*variant)
     n_nodes, n_time = 4096, 8192
     rng = np.random.default_rng(5)
     base = random_solve(rng, n_nodes, n_time, 2, it=False, ko=False)

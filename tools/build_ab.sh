@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build libfdcn.so from the csrc/ + include/ of a git revision (or the working
-# tree for "WT") into ab/TAG/libfdcn.so, for A/B timing through FDCN_LIB
-# (bench.py / capi.py).  Usage: bash tools/build_ab.sh TAG [REV]
+# tree for "WT") into ab/TAG/libfdcn.so, for A/B timing through bench.py --lib
+# (capi.LIB_PATH).  Usage: bash tools/build_ab.sh TAG [REV]
 set -euo pipefail
 TAG=$1; REV=${2:-WT}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 for rep in 1 2; do
   for wl in $WLS; do
     for t in $TAGS; do
-      FDCN_LIB=ab/$t/libfdcn.so timeout -k 10 200 python bench.py --workload $wl --no-cpu-baseline "$@" \
+      timeout -k 10 200 python bench.py --lib ab/$t/libfdcn.so --workload $wl --no-cpu-baseline "$@" \
           > gpurun_out/${OUT}_${wl}_${t}_${rep}.json 2>> gpurun_out/${OUT}.err || exit $?
     done
   done
