@@ -16,8 +16,18 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def pytest_addoption(parser):
+    parser.addoption("--fdcn-lib", default="",
+                     help="run against this build of libfdcn.so (the sanitizer build of "
+                          "`make sanitize`); default: the in-tree library")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: test needs an MI355X GPU and libfdcn.so")
+    alt = config.getoption("--fdcn-lib")
+    if alt:
+        from finite_difference_amd import capi
+        capi.LIB_PATH = os.path.abspath(alt)
 
 
 def load_golden(name):
