@@ -31,7 +31,118 @@ from typing import Dict, List, Literal, Optional, Tuple
 
 import numpy as np
 
+from . import capi
 from .engine import Engine, VcSolve, default_engine
+
+# ---------------------------------------------------------------------------
+# vectorised spot-grid helpers, shared with spot_barrier_analytic.py.  Every
+# elementwise expression keeps the reference's operand order, and Python's
+# float ** 2 / math.exp become libm pow / exp (capi.vmath), so the arrays are
+# bit-identical to the reference's list comprehensions (tests).
+# ---------------------------------------------------------------------------
+def _sq(x) -> np.ndarray:
+    """x ** 2 as CPython evaluates it (libm pow, not x * x)."""
+    x = np.asarray(x, np.float64)
+    return capi.vmath(capi.VM_SQUARE, x).reshape(x.shape)
+
+
+def nearest_node(nodes: np.ndarray, x: float) -> int:
+    """min(range(len(nodes)), key=lambda i: abs(nodes[i] - x)): first minimiser."""
+    return int(np.argmin(np.abs(nodes - x)))
+
+
+def uniform_spot_grid(s_max: float, n: int, snap=()) -> np.ndarray:
+    """s_min = 0 + i dS, i = 0..n, then each anchor in `snap` (None skipped)
+    written over its nearest node, in order."""
+    dS = (s_max - 0.0) / n
+    nodes = 0.0 + np.arange(n + 1, dtype=np.float64) * dS
+    for x in snap:
+        if x is not None:
+            nodes[nearest_node(nodes, x)] = float(x)
+    return nodes
+
+
+def smoothed_payoff(s: np.ndarray, strike: float, call: bool, half_width: int,
+                    keep_if_flat: bool) -> np.ndarray:
+    """Terminal payoff max(S - K, 0) / max(K - S, 0) with the quadratic
+    mollifier over the 2 half_width + 1 nodes around the strike node.  A
+    degenerate window (S1 == S0) leaves the payoff when keep_if_flat,
+    flattens it to V0 otherwise (the two reference pricers differ there)."""
+    e = s - strike if call else strike - s
+    V = np.where(0.0 > e, 0.0, e)  # Python max(e, 0.0)
+    if half_width <= 0:
+        return V
+    k = nearest_node(s, strike)
+    i0, i1 = max(0, k - half_width), min(len(s) - 1, k + half_width)
+    S0, V0, S1, V1 = float(s[i0]), float(V[i0]), float(s[i1]), float(V[i1])
+    if S1 != S0:
+        a = (V1 - V0) / float(_sq(S1 - S0))
+    elif keep_if_flat:
+        return V
+    else:
+        a = 0.0
+    V[i0:i1 + 1] = a * _sq(s[i0:i1 + 1] - S0) + V0
+    return V
+
+
+def theta_rows(s: np.ndarray, sig2S2: np.ndarray, dt: float, theta: float, r: float,
+               drift: float, explicit_sign: float) -> np.ndarray:
+    """[6, N+1] = sub, main, sup of A = I - theta dt L and a, b, c of the
+    explicit operator for interior rows 1..N-1 (rows 0 and N: the Dirichlet
+    identity), L the spot-space Black-Scholes operator with drift `drift`:
+      a = +-0.5 dt (1-theta) (sig2S2/dS^2 - drift S/dS), b = 1 - dt (1-theta) (sig2S2/dS^2 + r)
+    (discrete_barrier_fdm_pricer_2.py:354-417, discrete_barrier_analytic_pricer.py
+    :408-423); explicit_sign -1 is the reference's sign."""
+    N = len(s) - 1
+    dS = float(s[1] - s[0])
+    S = s[1:N]
+    x = sig2S2 / (dS ** 2)
+    y = drift * S / dS
+    D = np.zeros((6, N + 1))
+    D[1, 0] = D[1, N] = 1.0
+    D[0, 1:N] = -(0.5 * dt * theta * (x - y))
+    D[1, 1:N] = 1.0 + dt * theta * (x + r)
+    D[2, 1:N] = -(0.5 * dt * theta * (x + y))
+    D[3, 1:N] = explicit_sign * 0.5 * dt * (1 - theta) * (x - y)
+    D[4, 1:N] = 1.0 - dt * (1 - theta) * (x + r)
+    D[5, 1:N] = explicit_sign * 0.5 * dt * (1 - theta) * (x + y)
+    return D
+
+
+def interp_linear(x: float, xs: np.ndarray, ys) -> float:
+    """Clamped linear interpolation on a non-decreasing grid (the reference's
+    bisection: the bracket is [j, j+1] with j the last node <= x)."""
+    if x <= xs[0]:
+        return float(ys[0])
+    if x >= xs[-1]:
+        return float(ys[-1])
+    lo = int(np.searchsorted(xs, x, side="right")) - 1
+    x0, x1 = float(xs[lo]), float(xs[lo + 1])
+    y0, y1 = float(ys[lo]), float(ys[lo + 1])
+    w = (x - x0) / (x1 - x0)
+    return float((1 - w) * y0 + w * y1)
+
+
+def ko_thresholds(s: np.ndarray, barrier_type: str, lo_bar, up_bar) -> Tuple[int, int]:
+    """Integer thresholds (KO_LO, KO_HI) of the knock-out projection's
+    compares S <= lo_bar / S >= up_bar on the grid s (a non-decreasing
+    grid: every knocked-out node lies at or below KO_LO / at or above KO_HI;
+    checked)."""
+    n = len(s)
+    ko_lo, ko_hi = -1, n
+    if barrier_type in ("down-and-out", "double-out") and lo_bar is not None:
+        hit = s <= lo_bar
+        ko_lo = int(np.nonzero(hit)[0][-1]) if hit.any() else -1
+        if not hit[:ko_lo + 1].all():
+            raise ValueError("knock-out nodes are not a prefix of the grid")
+    if barrier_type in ("up-and-out", "double-out") and up_bar is not None:
+        hit = s >= up_bar
+        ko_hi = int(np.nonzero(hit)[0][0]) if hit.any() else n
+        if not hit[ko_hi:].all():
+            raise ValueError("knock-out nodes are not a suffix of the grid")
+    return ko_lo, ko_hi
+
+
 
 BarrierType = Literal["none", "down-and-out", "up-and-out", "double-out", "down-and-in",
                       "up-and-in", "double-in"]
@@ -126,27 +237,12 @@ class DiscreteBarrierFDMPricer2:
         """[0, 4 s_ref e^{sigma sqrt T}], N = max(200, num_space_nodes), K and
         the barriers snapped to their nearest nodes (:146-167)."""
         anchors = [self.spot_price, self.strike_price]
-        if self.barrier_lower:
-            anchors.append(self.barrier_lower)
-        if self.barrier_upper:
-            anchors.append(self.barrier_upper)
-        s_ref = max(anchors)
-        s_max = 4.0 * s_ref * math.exp(self.volatility * math.sqrt(max(self.tenor_years, 1e-12)))
-        s_min = 0.0
-        N = max(200, int(self.num_space_nodes))
-        dS = (s_max - s_min) / N
-        nodes = [s_min + i * dS for i in range(N + 1)]
-
-        def snap(x: Optional[float]):
-            if x is None:
-                return
-            j = min(range(len(nodes)), key=lambda i: abs(nodes[i] - x))
-            nodes[j] = float(x)
-
-        snap(self.strike_price)
-        snap(self.barrier_lower)
-        snap(self.barrier_upper)
-        return nodes
+        anchors += [b for b in (self.barrier_lower, self.barrier_upper) if b]
+        s_max = 4.0 * max(anchors) * math.exp(self.volatility *
+                                              math.sqrt(max(self.tenor_years, 1e-12)))
+        return uniform_spot_grid(s_max, max(200, int(self.num_space_nodes)),
+                                 (self.strike_price, self.barrier_lower,
+                                  self.barrier_upper)).tolist()
 
     def _decide_and_adjust_for_continuous_window(self):
         """FIS n_lim decision and BGK shift (:172-226)."""
@@ -182,106 +278,75 @@ class DiscreteBarrierFDMPricer2:
         k1 = max(0, min(self.num_time_steps, k1))
         return (frequent_enough, lo_adj, up_adj, min(k0, k1), max(k0, k1))
 
-    def _terminal_payoff_scalar(self, S: float) -> float:
-        if self.option_type == "call":
-            return max(S - self.strike_price, 0.0)
-        return max(self.strike_price - S, 0.0)
-
-    def _terminal_payoff_array(self, s_nodes: List[float]) -> List[float]:
-        V = [self._terminal_payoff_scalar(S) for S in s_nodes]
-        if not self.smooth_payoff_around_strike or self.payoff_smoothing_half_width_nodes <= 0:
-            return V
-        m = self.payoff_smoothing_half_width_nodes
-        k_star = min(range(len(s_nodes)), key=lambda i: abs(s_nodes[i] - self.strike_price))
-        i0, i1 = max(0, k_star - m), min(len(s_nodes) - 1, k_star + m)
-        S0, V0 = s_nodes[i0], V[i0]
-        S1, V1 = s_nodes[i1], V[i1]
-        a = (V1 - V0) / ((S1 - S0) ** 2) if S1 != S0 else 0.0
-        for i in range(i0, i1 + 1):
-            V[i] = a * (s_nodes[i] - S0) ** 2 + V0
-        return V
+    def _terminal_payoff_array(self, s_nodes) -> np.ndarray:
+        """Payoff with the strike mollifier (:231-249)."""
+        m = self.payoff_smoothing_half_width_nodes if self.smooth_payoff_around_strike else 0
+        return smoothed_payoff(np.asarray(s_nodes, np.float64), self.strike_price,
+                               self.option_type == "call", m, keep_if_flat=False)
 
     def _effective_barriers_for_pricing(self) -> Tuple[Optional[float], Optional[float]]:
         if self.use_bgk_correction:
             return self.bgk_lower, self.bgk_upper
         return self.barrier_lower, self.barrier_upper
 
-    def _locate_barrier_interval(self, s_nodes: List[float], lo_bar: Optional[float],
+    def _locate_barrier_interval(self, s_nodes, lo_bar: Optional[float],
                                  up_bar: Optional[float]):
         """(side, j, h_minus, h_plus) of the active knock-out barrier (:307-331)."""
-        N = len(s_nodes) - 1
+        s = np.asarray(s_nodes, np.float64)
+        N = len(s) - 1
         for side, kinds, H in (("down", ("down-and-out", "double-out"), lo_bar),
                                ("up", ("up-and-out", "double-out"), up_bar)):
             if self.barrier_type in kinds and H is not None:
-                if H <= s_nodes[0]:
-                    return (side, 0, 1e-12, s_nodes[1] - s_nodes[0])
-                if H >= s_nodes[-1]:
-                    return (side, N - 1, s_nodes[N - 1] - s_nodes[N - 2], 1e-12)
-                j = max(0, min(N - 1, next(k for k in range(N)
-                                           if s_nodes[k] <= H <= s_nodes[k + 1])))
-                return (side, j, max(1e-12, H - s_nodes[j]), max(1e-12, s_nodes[j + 1] - H))
+                if H <= s[0]:
+                    return (side, 0, 1e-12, float(s[1] - s[0]))
+                if H >= s[-1]:
+                    return (side, N - 1, float(s[N - 1] - s[N - 2]), 1e-12)
+                j = int(np.argmax((s[:-1] <= H) & (H <= s[1:])))  # first bracketing interval
+                return (side, j, max(1e-12, H - float(s[j])), max(1e-12, float(s[j + 1]) - H))
         return (None, None, None, None)
 
-    def _ko_nodes(self, s_nodes: List[float], lo_bar, up_bar) -> Tuple[int, int]:
+    def _ko_nodes(self, s_nodes, lo_bar, up_bar) -> Tuple[int, int]:
         """Integer thresholds equivalent to _apply_knockout_projection's
-        compares (:254-268) on the non-decreasing escrowed grid."""
-        s = np.asarray(s_nodes, dtype=np.float64)
-        ko_lo, ko_hi = -1, len(s_nodes)
-        if self.barrier_type in ("down-and-out", "double-out") and lo_bar is not None:
-            ko_lo = int(np.searchsorted(s, lo_bar, side="right")) - 1
-        if self.barrier_type in ("up-and-out", "double-out") and up_bar is not None:
-            ko_hi = int(np.searchsorted(s, up_bar, side="left"))
-        return ko_lo, ko_hi
+        compares (:254-268)."""
+        return ko_thresholds(np.asarray(s_nodes, np.float64), self.barrier_type, lo_bar, up_bar)
 
     def _apply_knockout_projection(self, values: List[float], lo_bar: Optional[float],
                                    up_bar: Optional[float], s_nodes: List[float]) -> None:
         """Host form of the projection (the kernel applies it in the march)."""
         lo, hi = self._ko_nodes(s_nodes, lo_bar, up_bar)
-        for i in range(len(s_nodes)):
-            if i <= lo or i >= hi:
-                values[i] = 0.0
+        for i in list(range(lo + 1)) + list(range(hi, len(s_nodes))):
+            values[i] = 0.0
 
     # ------------------------------------------------------------------ rows
-    def _rows(self, theta: float, s_nodes: List[float], side, j_bar, h_minus, h_plus) -> np.ndarray:
-        """sub, main, sup, a_expl, b_expl, c_expl of every row for one theta,
-        with the reference's expressions and operation order (:354-417)."""
-        N = len(s_nodes) - 1
+    def _rows(self, theta: float, s_nodes, side, j_bar, h_minus, h_plus) -> np.ndarray:
+        """sub, main, sup, a_expl, b_expl, c_expl of every row for one theta
+        (:354-417): the uniform rows vectorised (theta_rows), then the two
+        non-symmetric rows beside the barrier from its one-sided
+        three-point stencil."""
+        s = np.asarray(s_nodes, np.float64)
+        N = len(s) - 1
         dt, r, sig = self.dt, self.r_flat, self.volatility
-        dS = s_nodes[1] - s_nodes[0]
         sgn = 1.0 if self.explicit_sign == "corrected" else -1.0
-        D = np.zeros((6, N + 1))
-        D[1, 0] = 1.0
-        D[1, N] = 1.0
-        for i in range(1, N):
-            S = s_nodes[i]
-            sig2S2 = (sig * S) ** 2
-            if side is None or i not in (j_bar, j_bar + 1):
-                a_impl = 0.5 * dt * theta * (sig2S2 / (dS ** 2) - r * S / dS)
-                b_impl = 1.0 + dt * theta * (sig2S2 / (dS ** 2) + r)
-                c_impl = 0.5 * dt * theta * (sig2S2 / (dS ** 2) + r * S / dS)
-                a_expl = sgn * 0.5 * dt * (1 - theta) * (sig2S2 / (dS ** 2) - r * S / dS)
-                b_expl = 1.0 - dt * (1 - theta) * (sig2S2 / (dS ** 2) + r)
-                c_expl = sgn * 0.5 * dt * (1 - theta) * (sig2S2 / (dS ** 2) + r * S / dS)
-            else:
-                hm = float(h_minus)
-                hp = float(h_plus)
-                a1 = hp / (hm * (hm + hp))
-                b1 = (hp - hm) / (hm * hp)
-                c1 = -hm / (hp * (hm + hp))
-                d2 = 2.0 / (hm * (hm + hp))
-                e2 = -2.0 / (hm * hp)
-                f2 = 2.0 / (hp * (hm + hp))
+        D = theta_rows(s, _sq(sig * s[1:N]), dt, theta, r, r, sgn)
+        if side is not None:
+            hm, hp = float(h_minus), float(h_plus)
+            a1 = hp / (hm * (hm + hp))
+            b1 = (hp - hm) / (hm * hp)
+            c1 = -hm / (hp * (hm + hp))
+            d2 = 2.0 / (hm * (hm + hp))
+            e2 = -2.0 / (hm * hp)
+            f2 = 2.0 / (hp * (hm + hp))
+            for i in (j_bar, j_bar + 1):
+                if not 1 <= i <= N - 1:
+                    continue
+                S = float(s[i])
+                sig2S2 = float(_sq(sig * S))
                 L_left = 0.5 * sig2S2 * f2 + r * S * c1
                 L_center = 0.5 * sig2S2 * e2 + r * S * b1 - r
                 L_right = 0.5 * sig2S2 * d2 + r * S * a1
-                a_impl = -theta * dt * L_left
-                b_impl = 1.0 - theta * dt * L_center
-                c_impl = -theta * dt * L_right
-                a_expl = (1 - theta) * dt * L_left
-                b_expl = 1.0 + (1 - theta) * dt * L_center
-                c_expl = (1 - theta) * dt * L_right
-            D[0, i], D[1, i], D[2, i] = -a_impl, b_impl, -c_impl
-            D[3, i], D[4, i], D[5, i] = a_expl, b_expl, c_expl
+                D[:, i] = (theta * dt * L_left, 1.0 - theta * dt * L_center,
+                           theta * dt * L_right, (1 - theta) * dt * L_left,
+                           1.0 + (1 - theta) * dt * L_center, (1 - theta) * dt * L_right)
         return D
 
     def _monitoring_step_map(self) -> Dict[int, bool]:
@@ -308,16 +373,16 @@ class DiscreteBarrierFDMPricer2:
         r_steps = min(self.rannacher_steps, M)
         diag = np.stack([self._rows(1.0, s_nodes, side, j_bar, h_minus, h_plus),
                          self._rows(0.5, s_nodes, side, j_bar, h_minus, h_plus)])
+        # Dirichlet rows at tau_left = T - (m - 1) dt, m = M - k
+        tau_left = self.tenor_years - (M - np.arange(M) - 1).astype(np.float64) * self.dt
+        disc_K = self.strike_price * capi.vmath(capi.VM_EXP, -self.r_flat * tau_left)
         bnd = np.zeros((M, 2))
-        for k in range(M):
-            m = M - k
-            tau_left = self.tenor_years - (m - 1) * self.dt
-            if self.option_type == "call":
-                bnd[k] = (0.0, s_nodes[-1] - self.strike_price * math.exp(-self.r_flat * tau_left))
-            else:
-                bnd[k] = (self.strike_price * math.exp(-self.r_flat * tau_left), 0.0)
+        if self.option_type == "call":
+            bnd[:, 1] = s_nodes[-1] - disc_K
+        else:
+            bnd[:, 0] = disc_K
         sv = VcSolve(n_time=M, n_ranna=r_steps, diag=diag, bnd=bnd,
-                     v_init=np.asarray(self._terminal_payoff_array(s_nodes), dtype=np.float64))
+                     v_init=self._terminal_payoff_array(s_nodes))
         if monitor_step_index:
             steps = sorted(M - q for q in monitor_step_index if 0 <= q <= M - 1)
             if steps:
@@ -334,28 +399,15 @@ class DiscreteBarrierFDMPricer2:
                                                   s_nodes)])[0].tolist()
 
     @staticmethod
-    def _interp_linear(x: float, xs: List[float], ys: List[float]) -> float:
-        if x <= xs[0]:
-            return float(ys[0])
-        if x >= xs[-1]:
-            return float(ys[-1])
-        lo, hi = 0, len(xs) - 1
-        while hi - lo > 1:
-            mid = (lo + hi) // 2
-            if x < xs[mid]:
-                hi = mid
-            else:
-                lo = mid
-        x0, x1 = xs[lo], xs[hi]
-        y0, y1 = ys[lo], ys[hi]
-        w = (x - x0) / (x1 - x0)
-        return float((1 - w) * y0 + w * y1)
+    def _interp_linear(x: float, xs, ys) -> float:
+        return interp_linear(x, np.asarray(xs, np.float64), ys)
 
     # ----------------------------------------------------------- public API
     def _grid_solves(self) -> Tuple[List[float], float, List[VcSolve]]:
         pv_divs = self._pv_dividends_escrow()
         S_eff = self.spot_price - pv_divs
-        S_shifted = [max(s - pv_divs, 0.0) for s in self.S_nodes]
+        e = np.asarray(self.S_nodes, np.float64) - pv_divs
+        S_shifted = np.where(0.0 > e, 0.0, e).tolist()  # max(s - pv, 0.0)
         lo_eff, up_eff = self._effective_barriers_for_pricing()
         mp = self._monitoring_step_map()
         solves = [self._solve(lo_eff, up_eff, mp, S_shifted)]
@@ -365,11 +417,9 @@ class DiscreteBarrierFDMPricer2:
 
     @staticmethod
     def _combine(barrier_type: str, res: List[np.ndarray]) -> List[float]:
-        V = res[0].tolist()
         if barrier_type in ("down-and-in", "up-and-in", "double-in"):
-            Vv = res[1].tolist()
-            V = [Vv[i] - V[i] for i in range(len(V))]
-        return V
+            return (res[1] - res[0]).tolist()  # vanilla - knock-out
+        return res[0].tolist()
 
     def _solve_grid_once(self) -> Tuple[List[float], List[float], float]:
         """(S_grid_shifted, V_grid, effective spot) (:467-481)."""
@@ -385,7 +435,7 @@ class DiscreteBarrierFDMPricer2:
         """FIS Greeks stencils (:488-550)."""
         N = len(s_nodes) - 1
         dS = s_nodes[1] - s_nodes[0]
-        iS = max(1, min(N - 1, min(range(N), key=lambda k: abs(S_eff - s_nodes[k]))))
+        iS = max(1, min(N - 1, nearest_node(np.asarray(s_nodes[:N], np.float64), S_eff)))
         delta_c = (V[iS + 1] - V[iS - 1]) / (2.0 * dS)
         gamma_c = (V[iS + 1] - 2.0 * V[iS] + V[iS - 1]) / (dS * dS)
         side, j_bar, h_minus, h_plus = self._locate_barrier_interval(s_nodes, lo_bar, up_bar)
