@@ -233,6 +233,17 @@ class HipBackend:
         return capi.vc_batch(g.n_nodes, g.n_time, g.n_ranna, g.diag, g.bnd, g.v_init,
                              g.iparams, g.mon_step, g.mon_rebate)
 
+    def run_rr(self, contracts) -> np.ndarray:
+        """BarrierEngine(**c).price() of every contract (fdcn_rr_barrier_batch)."""
+        from .analytic import barrier_engine_batch
+        return barrier_engine_batch(contracts)[0]
+
+    def run_double(self, contracts, m: int) -> np.ndarray:
+        """DoubleBarrier(..., m).price(b, r, T) of every contract
+        (fdcn_double_barrier_batch)."""
+        from .analytic import double_barrier_batch
+        return double_barrier_batch(contracts, m)
+
     def run_group(self, g: Group) -> np.ndarray:
         if g.it:
             return capi.it_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams,
@@ -318,6 +329,16 @@ class Engine:
             for row, i in enumerate(g.index):
                 out[i] = res[row]
         return out  # type: ignore[return-value]
+
+    def run_rr(self, contracts) -> np.ndarray:
+        """Closed-form single-barrier prices (one batched launch)."""
+        self.launches += 1
+        return np.asarray(self.backend.run_rr(list(contracts)), np.float64)
+
+    def run_double(self, contracts, m: int) -> np.ndarray:
+        """Closed-form double-barrier prices, series n = -m..m (one launch)."""
+        self.launches += 1
+        return np.asarray(self.backend.run_double(list(contracts), int(m)), np.float64)
 
     def run(self, solves: Sequence[Solve]) -> List[np.ndarray]:
         out: List[Optional[np.ndarray]] = [None] * len(solves)

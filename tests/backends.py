@@ -28,5 +28,21 @@ class OracleBackend:
                                g.iparams, g.mon_step, g.mon_rebate, self.nthreads)
 
 
+    def run_rr(self, contracts):
+        """The host closed form (analytic.BarrierEngine, the reference's
+        formulas in NumPy/SciPy) in place of the GPU batch."""
+        from finite_difference_amd.analytic import BarrierEngine
+        return [BarrierEngine(**c).price() for c in contracts]
+
+    def run_double(self, contracts, m):
+        from finite_difference_amd.analytic import DoubleBarrier
+        out = []
+        for c in contracts:
+            c = dict(c)
+            b, r, T = c.pop("b"), c.pop("r"), c.pop("T")
+            out.append(DoubleBarrier(m=m, **c).price(b=b, r=r, T=T))
+        return out
+
+
 def oracle_engine() -> Engine:
     return Engine(OracleBackend())

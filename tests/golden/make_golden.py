@@ -517,9 +517,120 @@ def gen_analytic():
     dump("analytic_cases.json", dict(barrier_engine=rows, double_barrier=dbl))
 
 
+def gen_spot_analytic():
+    """DiscreteBarrierFDMPricerAnalytic (discrete_barrier_analytic_pricer.py):
+    the FIS n_lim decision, the BGK-shifted analytic engines on the continuous
+    window (barrier_engine.BarrierEngine; DoubleBarrier), the CN overlay with
+    knock-out on discrete monitoring steps or on every step of the window,
+    knock-ins as CN vanilla minus the knock-out leg, bump-and-reprice Greeks.
+
+    The module imports ``from double_barrier import DoubleBarrier``; the
+    reference's file is "double _barrier.py" (a space in the name), so as
+    shipped DoubleBarrier is None and the double-barrier continuous branch
+    falls back to the CN overlay.  Cases marked ``douady`` bind the module's
+    DoubleBarrier to "double _barrier.py" (what the import intends); the
+    others run the module as shipped."""
+    import pandas as pd
+    sys.path.insert(0, REF)
+    import discrete_barrier_analytic_pricer as m  # type: ignore
+    shipped_db = m.DoubleBarrier
+    assert shipped_db is None, "expected the shipped import of double_barrier to fail"
+    v0, v1 = pd.Timestamp("2025-07-28"), pd.Timestamp("2026-01-28")
+    daily = [v0 + pd.Timedelta(days=i) for i in range(1, 185)]
+    weekly = [v0 + pd.Timedelta(days=7 * i) for i in range(1, 27)]
+    monthly = [v0 + pd.Timedelta(days=30 * i) for i in range(1, 7)]
+    base = dict(trade_id="T1", direction="long", quantity=1, contract_multiplier=1.0,
+                valuation_date=v0, maturity_date=v1)
+    specs = [
+        dict(name="put_do_weekly_cn", option_type="put", barrier_type="down-and-out",
+             strike=105.0, lower_barrier=85.0, upper_barrier=None, spot=100.0, volatility=0.3,
+             monitoring_dates=weekly, rate=0.06, time_steps=8, space_nodes=150),
+        dict(name="call_uo_monthly_cn_short", option_type="call", barrier_type="up-and-out",
+             strike=95.0, lower_barrier=None, upper_barrier=125.0, spot=100.0, volatility=0.22,
+             monitoring_dates=monthly, rate=0.05, time_steps=6, space_nodes=160,
+             direction="short", quantity=10, contract_multiplier=2.0),
+        dict(name="call_uo_daily_rr", option_type="call", barrier_type="up-and-out",
+             strike=100.0, lower_barrier=None, upper_barrier=130.0, spot=100.0,
+             volatility=0.25, monitoring_dates=daily, rate=0.05, time_steps=10,
+             space_nodes=150, n_desired_for_decision=20, rebate_amount=1.5,
+             rebate_timing_out="expiry"),
+        dict(name="put_di_daily_rr", option_type="put", barrier_type="down-and-in",
+             strike=100.0, lower_barrier=85.0, upper_barrier=None, spot=100.0, volatility=0.3,
+             monitoring_dates=daily, rate=0.05, time_steps=8, space_nodes=140,
+             n_desired_for_decision=20, divs=[("2025-10-15", 1.5)]),
+        dict(name="call_ui_weekly_cn_divs", option_type="call", barrier_type="up-and-in",
+             strike=98.0, lower_barrier=None, upper_barrier=120.0, spot=100.0, volatility=0.2,
+             monitoring_dates=weekly, rate=0.07, time_steps=6, space_nodes=150,
+             divs=[("2025-09-01", 1.0), ("2025-12-01", 1.25)]),
+        dict(name="call_uo_daily_crossed_cn", option_type="call", barrier_type="up-and-out",
+             strike=100.0, lower_barrier=None, upper_barrier=130.0, spot=100.0,
+             volatility=0.25, monitoring_dates=daily, rate=0.05, time_steps=8, space_nodes=150,
+             n_desired_for_decision=20, barrier_status="not_crossed"),
+        dict(name="dko_daily_cn", option_type="call", barrier_type="double-out", strike=100.0,
+             lower_barrier=80.0, upper_barrier=125.0, spot=100.0, volatility=0.2,
+             monitoring_dates=daily, rate=0.05, time_steps=6, space_nodes=150,
+             n_desired_for_decision=20),
+        dict(name="dko_daily_douady", douady=True, option_type="call", barrier_type="double-out",
+             strike=100.0, lower_barrier=80.0, upper_barrier=125.0, spot=100.0, volatility=0.2,
+             monitoring_dates=daily, rate=0.05, time_steps=6, space_nodes=150,
+             n_desired_for_decision=20),
+        dict(name="put_dki_daily_douady", douady=True, option_type="put",
+             barrier_type="double-in", strike=100.0, lower_barrier=82.0, upper_barrier=120.0,
+             spot=100.0, volatility=0.2, monitoring_dates=daily, rate=0.05, time_steps=6,
+             space_nodes=150, n_desired_for_decision=20),
+        dict(name="vanilla_put", option_type="put", barrier_type="none", strike=100.0,
+             lower_barrier=None, upper_barrier=None, spot=100.0, volatility=0.25,
+             monitoring_dates=[], rate=0.05, time_steps=6, space_nodes=150,
+             snap_strike_and_barrier=False),
+    ]
+    cases = []
+    for sp in specs:
+        kw = dict(base)
+        kw.update({k: v for k, v in sp.items() if k not in ("name", "rate", "divs", "douady")})
+        c = curve(sp["rate"])
+        kw["discount_curve"] = c
+        kw["forward_curve"] = c
+        kw["dividend_schedule"] = [(pd.Timestamp(d), a) for d, a in sp.get("divs", [])]
+        m.DoubleBarrier = load_double_barrier().DoubleBarrier if sp.get("douady") else shipped_db
+        try:
+            p = m.DiscreteBarrierFDMPricerAnalytic(**kw)
+            rec = dict(name=sp["name"],
+                       inputs={k: ([str(d.date()) for d in v] if k == "monitoring_dates" else v)
+                               for k, v in sp.items()},
+                       spot_grid=list(p.spot_grid), flat_rate_r=p.flat_rate_r,
+                       flat_dividend_q=p.flat_dividend_q,
+                       use_continuous_window=p.use_continuous_window,
+                       window=[p.window_k0, p.window_k1],
+                       bgk=[p.bgk_lower_barrier, p.bgk_upper_barrier],
+                       monitor_discrete=sorted(p.monitor_steps_discrete),
+                       monitor_continuous=sorted(p.monitor_steps_continuous))
+            # the value vectors price() marches (escrowed grid)
+            S_eff = p._escrowed_spot()
+            grid0 = p.spot_grid[:]
+            p.spot_grid = [max(0.0, s - (p.spot - S_eff)) for s in grid0]
+            p.grid_step_dS = p.spot_grid[1] - p.spot_grid[0]
+            rec["S_eff"] = S_eff
+            rec["grid_escrowed"] = list(p.spot_grid)
+            rec["V_discrete"] = p._cn_stepper(p.lower_barrier, p.upper_barrier,
+                                              p.monitor_steps_discrete)
+            rec["V_vanilla"] = p._cn_stepper(None, None, {})
+            if p.monitor_steps_continuous:
+                rec["V_continuous"] = p._cn_stepper(p.bgk_lower_barrier, p.bgk_upper_barrier,
+                                                    p.monitor_steps_continuous)
+            p.spot_grid = grid0
+            p.grid_step_dS = p.spot_grid[1] - p.spot_grid[0]
+            rec["price"] = p.price()
+            rec["greeks"] = p.greeks()
+        finally:
+            m.DoubleBarrier = shipped_db
+        cases.append(rec)
+    dump("spot_analytic_cases.json", dict(curve_rates={c["name"]: c["rate"] for c in specs},
+                                          cases=cases))
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["cn", "barrier", "double", "spot", "american", "analytic",
-                             "black76"]
+                             "black76", "spot_analytic"]
     if "black76" in which:
         gen_black76()
     if "cn" in which:
@@ -534,3 +645,5 @@ if __name__ == "__main__":
         gen_american(with_config2="config2" in which or not sys.argv[1:])
     if "analytic" in which:
         gen_analytic()
+    if "spot_analytic" in which:
+        gen_spot_analytic()

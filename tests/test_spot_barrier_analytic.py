@@ -1,0 +1,174 @@
+"""DiscreteBarrierFDMPricerAnalytic (second entry point):
+the FIS n_lim decision, BGK-shifted closed forms on the continuous window, the
+spot-space CN overlay (discrete monitoring, or projection on every step of the
+window), knock-ins by parity, bump-and-reprice Greeks.
+
+Fixtures: tests/golden/spot_analytic_cases.json, produced by the reference
+module itself (tests/golden/make_golden.py gen_spot_analytic), including its
+wrong-sign explicit terms (:416-418, so the CN values grow large; they are
+still the reference's values) and, for the cases marked douady, its intended
+DoubleBarrier import bound to "double _barrier.py".
+
+CPU: the facade with the C oracle as its CN backend and the host closed forms
+(analytic.py) as its analytic backend:
+  * decision, BGK barriers, monitoring maps, flat r / q, grids: bitwise;
+  * every CN value vector (discrete, vanilla, continuous window): bitwise;
+  * price / Greeks of the CN-only cases: bitwise;
+  * cases with a closed-form leg: the host engines match the reference's to
+    1e-12 relative (test_analytic.py), so price 1e-11 relative, Delta 1e-8
+    absolute, vega 1e-6, Gamma (a /ds^2 of a price difference) 1e-5.
+GPU: the product engine (fdcn_vc_batch + the batched closed forms) against
+the oracle-driven facade on the same trades: CN vectors 1e-9 relative to each
+vector's magnitude (the reference-sign growth amplifies rounding), prices
+and Greeks with the bounds above scaled by that growth.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from backends import oracle_engine
+from conftest import load_golden
+from finite_difference_amd.engine import Engine
+from finite_difference_amd.spot_barrier_analytic import DiscreteBarrierFDMPricerAnalytic
+
+GOLD = load_golden("spot_analytic_cases.json")
+CASES = GOLD["cases"]
+
+
+def make(case, engine, **extra):
+    import pandas as pd
+    from finite_difference_amd import market
+    inp = dict(case["inputs"])
+    inp.pop("name")
+    rate = inp.pop("rate")
+    divs = inp.pop("divs", [])
+    douady = inp.pop("douady", False)
+    c = market.create_rate_df(rate)
+    c["Date"] = pd.to_datetime(c["Date"], format="%Y/%m/%d").dt.strftime("%Y-%m-%d")
+    kw = dict(trade_id="T1", direction="long", quantity=1, contract_multiplier=1.0,
+              valuation_date=pd.Timestamp("2025-07-28"), maturity_date=pd.Timestamp("2026-01-28"),
+              discount_curve=c, forward_curve=c,
+              dividend_schedule=[(pd.Timestamp(d), a) for d, a in divs],
+              double_barrier_analytic=douady, engine=engine)
+    kw.update(inp)
+    kw["monitoring_dates"] = [pd.Timestamp(d) for d in inp["monitoring_dates"]]
+    kw.update(extra)
+    return DiscreteBarrierFDMPricerAnalytic(**kw)
+
+
+def _analytic_leg(p) -> bool:
+    if not p.use_continuous_window:
+        return False
+    return p._continuous_leg(p.spot, p.sigma)[0] != "cn"
+
+
+def _vectors(p):
+    """The value vectors price() marches, by the product's own solve builder."""
+    out = {}
+    for which in ("discrete", "vanilla", "continuous"):
+        if which == "continuous" and not p.monitor_steps_continuous:
+            continue
+        S_eff = p.spot - p._pv_dividends()
+        out[which] = p._cn_for_key((p.sigma, p.spot - S_eff, which))
+    return out
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["name"])
+def test_decision_grid_and_curves_bitwise(case):
+    p = make(case, oracle_engine())
+    assert p.spot_grid == case["spot_grid"]
+    assert p.flat_rate_r == case["flat_rate_r"]
+    assert p.flat_dividend_q == case["flat_dividend_q"]
+    assert p.use_continuous_window == case["use_continuous_window"]
+    assert [p.window_k0, p.window_k1] == case["window"]
+    assert [p.bgk_lower_barrier, p.bgk_upper_barrier] == case["bgk"]
+    assert sorted(p.monitor_steps_discrete) == case["monitor_discrete"]
+    assert sorted(p.monitor_steps_continuous) == case["monitor_continuous"]
+    S_eff = p.spot - p._pv_dividends()
+    assert S_eff == case["S_eff"]
+    assert p._escrowed_grid(p.spot - S_eff).tolist() == case["grid_escrowed"]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["name"])
+def test_cn_stepper_vectors_bitwise(case):
+    p = make(case, oracle_engine())
+    solves = _vectors(p)
+    got = dict(zip(solves, oracle_engine().run_vc(list(solves.values()))))
+    assert got["discrete"].tolist() == case["V_discrete"]
+    assert got["vanilla"].tolist() == case["V_vanilla"]
+    if "V_continuous" in case:
+        assert got["continuous"].tolist() == case["V_continuous"]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["name"])
+def test_price_and_greeks_vs_reference(case):
+    p = make(case, oracle_engine())
+    price, greeks = p.price(), p.greeks()
+    if not _analytic_leg(p):
+        assert price == case["price"]
+        assert greeks == case["greeks"]
+        return
+    ref, g = case["price"], case["greeks"]
+    assert math.isclose(price, ref, rel_tol=1e-11, abs_tol=1e-12), (price, ref)
+    assert abs(greeks["delta"] - g["delta"]) <= 1e-8 * max(1.0, abs(ref))
+    assert abs(greeks["vega"] - g["vega"]) <= 1e-6 * max(1.0, abs(ref))
+    assert abs(greeks["gamma"] - g["gamma"]) <= 1e-5 * max(1.0, abs(ref))
+
+
+def test_greeks_march_once_per_distinct_grid():
+    """greeks(): five repricings, but the spot bumps only move the
+    interpolation point -- without dividends the CN legs need the base and
+    the two sigma-bumped grids, all in one launch."""
+    case = next(c for c in CASES if c["name"] == "put_do_weekly_cn")
+    eng = oracle_engine()
+    p = make(case, eng)
+    before = (eng.launches, eng.solves)
+    p.greeks()
+    assert (eng.launches - before[0], eng.solves - before[1]) == (1, 3)
+
+
+def test_validation_errors():
+    case = CASES[0]
+    with pytest.raises(ValueError):
+        make(case, None, spot=-1.0)
+    with pytest.raises(ValueError):
+        make(case, None, explicit_sign="other")
+    import pandas as pd
+    with pytest.raises(ValueError):
+        make(case, None, maturity_date=pd.Timestamp("2025-07-01"))
+
+
+def test_corrected_sign_vanilla_converges_to_black_scholes():
+    from finite_difference_amd.analytic import black_scholes
+    case = next(c for c in CASES if c["name"] == "vanilla_put")
+    p = make(case, oracle_engine(), explicit_sign="corrected", time_steps=400, space_nodes=800)
+    ref = float(black_scholes("p", 100.0, 100.0, p.flat_rate_r, p.flat_carry_b, 0.25,
+                              p.tenor_years))
+    assert abs(p.price() - ref) < 1e-2 * ref, (p.price(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["name"])
+def test_gpu_facade_vs_oracle_facade(case):
+    gpu, ref = make(case, Engine()), make(case, oracle_engine())
+    for which, sv in _vectors(gpu).items():
+        g = Engine().run_vc([sv])[0]
+        r = oracle_engine().run_vc([sv])[0]
+        assert np.max(np.abs(g - r)) <= 1e-9 * max(1.0, float(np.max(np.abs(r)))), which
+    growth = max(1.0, max(abs(x) for x in case["V_vanilla"]))
+    pg, pr = gpu.price(), ref.price()
+    assert abs(pg - pr) <= 1e-9 * growth, (pg, pr)
+    gg, gr = gpu.greeks(), ref.greeks()
+    assert abs(gg["delta"] - gr["delta"]) <= 1e-7 * growth
+    assert abs(gg["vega"] - gr["vega"]) <= 1e-5 * growth
+    assert abs(gg["gamma"] - gr["gamma"]) <= 1e-3 * growth
+
+
+@pytest.mark.gpu
+def test_gpu_corrected_knock_out_between_zero_and_vanilla():
+    case = next(c for c in CASES if c["name"] == "put_do_weekly_cn")
+    ko = make(case, Engine(), explicit_sign="corrected", time_steps=300, space_nodes=600)
+    van = make(dict(case, inputs=dict(case["inputs"], barrier_type="none")), Engine(),
+               explicit_sign="corrected", time_steps=300, space_nodes=600)
+    assert 0.0 < ko.price() < van.price()
