@@ -184,3 +184,28 @@ def test_concurrent_groups_reuse_the_launch_threads():
     finally:
         capi.current_device, capi.select_device = saved
     assert 1 <= len(be.threads) <= 8
+
+
+def test_one_hip_runtime_after_load():
+    """capi.lib() preloads torch's HIP runtime only when its SONAME
+    is the one libfdcn needs, so the process maps exactly one
+    libamdhip64 (checked in a fresh interpreter: this one may have loaded
+    other builds)."""
+    import subprocess
+    import sys
+    code = ("from finite_difference_amd import capi; capi.lib(); import torch; "
+            "maps = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}; "
+            "print(len(maps), sorted(maps))")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(capi.__file__)))
+    assert p.returncode == 0, p.stderr[-2000:]
+    n = int(p.stdout.split()[0])
+    assert n == 1, p.stdout
+
+
+def test_elf_dynamic_names_reads_needed_and_soname():
+    names = capi.elf_dynamic_names(capi.LIB_PATH)
+    assert any(n.startswith("libamdhip64.so") for n in names["needed"])
+    torch_rt = capi._torch_hip_runtime()
+    if torch_rt:
+        assert capi.elf_dynamic_names(torch_rt)["soname"].startswith("libamdhip64.so")
