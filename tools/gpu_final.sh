@@ -15,6 +15,14 @@ timeout -k 10 300 python bench.py > $O/bench_american.json 2> $O/bench_american.
 for wl in barrier double analytic scenario_file american_file trade_cnlog trade_american trade_double; do
   timeout -k 10 300 python bench.py --workload $wl > $O/bench_$wl.json 2> $O/bench_$wl.err || exit $?
 done
+# BASELINE config 4: one 10 000-scenario batch; the per-rank batch sizes of
+# its 2/4/8-GPU shards on this one GPU
+timeout -k 10 300 python bench.py --workload barrier --total 10000 > $O/bench_barrier_total.json \
+    2> $O/bench_barrier_total.err || exit $?
+for B in 1250 2500 5000; do
+  timeout -k 10 300 python bench.py --workload barrier --batch $B --no-cpu-baseline \
+      > $O/bench_barrier_b$B.json 2> $O/bench_barrier_b$B.err || exit $?
+done
 for wl in american barrier double; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o $wl -- \
       python3 bench.py --workload $wl --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_$wl.log 2>&1 || exit $?
