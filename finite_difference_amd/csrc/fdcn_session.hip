@@ -371,8 +371,12 @@ struct PinnedArena {
     chunks.resize(k);
   }
 };
-// pinned staging an idle per-thread context keeps between sessions
-constexpr size_t kIdlePinnedBytes = size_t(64) << 20;
+// pinned staging an idle per-thread context keeps between sessions: enough
+// for a whole-file plan (a 10 000-row barrier file stages 131 MB, a 2 000-row
+// American file ~400 MB), so repeated files reuse it (pinning it again costs
+// ~15-40 ms per file: 34 -> 52 ms per 10 000-row file with a 64 MB cap),
+// while the process's locked memory stays bounded per thread
+constexpr size_t kIdlePinnedBytes = size_t(1) << 30;
 
 // Per-thread, per-device resources a session borrows: streams, spare events
 // and the pinned arena.  Creating them costs far more than a small trade's
