@@ -124,6 +124,26 @@ __device__ __forceinline__ double dpp_move(double x) {
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
   return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
+// acc += bcast(tab, lane i of each 16-lane row) * c: a per-scenario table
+// value (the same on every lane of the wave) broadcast by 64-bit DPP
+// (row_newbcast) straight into the FMA -- no LDS read, no register holding
+// the value.  The table sits in one VGPR pair, lane l holding entry l mod
+// 16.  i is a compile-time constant after unrolling (the switch folds away).
+__device__ __forceinline__ void fmac_bcast(double& acc, double tab, double c, int i) {
+  switch (i) {
+#define FDCN_BC(n)                                                                        \
+  case n:                                                                                 \
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #n " row_mask:0xf bank_mask:0xf" \
+                 : "+v"(acc) : "v"(tab), "v"(c));                                         \
+    break;
+    FDCN_BC(0) FDCN_BC(1) FDCN_BC(2) FDCN_BC(3) FDCN_BC(4) FDCN_BC(5) FDCN_BC(6) FDCN_BC(7)
+    FDCN_BC(8) FDCN_BC(9) FDCN_BC(10) FDCN_BC(11) FDCN_BC(12) FDCN_BC(13) FDCN_BC(14)
+    FDCN_BC(15)
+#undef FDCN_BC
+    default: break;
+  }
+}
+
 constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1
 constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1
 __device__ __forceinline__ double shfl_up1(double x, int d) {
@@ -364,8 +384,11 @@ __host__ __device__ constexpr int sub_chains(int it, int w, int npt, int zg) {
 // its update reads two tables per node against one, and at its 128-register
 // cap the prefetch spilled (10.9 ms against 5.5; 6.0 with S = 2 at three
 // waves per SIMD), so it keeps the re-run passes.
+// Round 3: the one-wave split-form CN variants up to 16 nodes per lane
+// (config 3) run two-pass too, with the homogeneous tables as DPP
+// broadcasts (fmac_bcast) instead of the LDS reads that lost in round 2.
 __host__ __device__ constexpr bool two_pass(int it, int w, int npt, int zg) {
-  return it && w == 1 && zg == 0 && npt >= 2;
+  return w == 1 && zg == 0 && npt >= 2 && (it || npt <= 16);
 }
 
 // Doubles of the correction tables per scenario.  Two-pass variants: per
@@ -706,7 +729,10 @@ fdcn_march(KArgs A) {
   static_assert(!(kRec && kSplit), "one step form per variant");
   // two-pass solve (see two_pass): tables per phase at ztab + tab * kTPh
   constexpr bool kTP = two_pass(IT, W, NPT, ZG);
-  static_assert(!kTP || (IT && M >= 2 && !kPair), "two-pass: IT, one scenario per wave, M >= 2");
+  // the split-form CN on the two-pass solve, tables as DPP broadcasts
+  constexpr bool kTPS = kTP && !IT;
+  static_assert(!kTP || (M >= 2 && !kPair), "two-pass: one scenario per wave, M >= 2");
+  static_assert(!kTPS || (kSplit && S == 1 && M <= 16), "split two-pass: S = 1, M <= 16");
   const int kTPh = kTP ? 2 * M + lz * 2 * S : 0;  // doubles per phase
   // per sub-chain coefficients of the homogeneous part (two-pass solve), the
   // solution's value at the chunk's first node after the backward scan, and
@@ -1089,7 +1115,8 @@ fdcn_march(KArgs A) {
     for (int j = 1; j < S; ++j) e = fma(j == S - 1 ? mulLF : fmM, e, a[j]);
     double b = e;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b = fma(FW[j], scan_up(b, 1 << j, lane4), b);
+    for (int j = 0; j < 2; ++j)
+      if (!kSplit || j < nst_f) b = fma(FW[j], scan_up(b, 1 << j, lane4), b);
     if (nst_f > 2) {
 #pragma unroll
       for (int j = 2; j < 6; ++j) {
@@ -1116,7 +1143,9 @@ fdcn_march(KArgs A) {
 #pragma unroll
       for (int i = M - 2; i >= 0; --i) {
         const int k = j * M + i;
-        y = fma(k == NPT - 2 ? bw1l : bm, y, Wr(k));
+        // a sub-chain's first node: its zero-carry forward value is its
+        // input (kSplit: not copied into T by the forward pass)
+        y = fma(k == NPT - 2 ? bw1l : bm, y, i == 0 ? In(k) : Wr(k));
         Wr(k) = y;
       }
       // the sub-chain's start value with its forward carry, zero backward carry
@@ -1128,7 +1157,8 @@ fdcn_march(KArgs A) {
     for (int j = S - 2; j >= 0; --j) e = fma(bmM, e, a[j]);
     double cb = e;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) cb = fma(GW[j], scan_dn(cb, 1 << j, lane4), cb);
+    for (int j = 0; j < 2; ++j)
+      if (!kSplit || j < nst_b) cb = fma(GW[j], scan_dn(cb, 1 << j, lane4), cb);
     if (nst_b > 2) {
 #pragma unroll
       for (int j = 2; j < 6; ++j) {
@@ -1396,6 +1426,18 @@ fdcn_march(KArgs A) {
     return kTP ? lds_addr(ztab + tb_ * kTPh + 2 * M + (t < lz ? t : lz - 1) * 2 * S) : 0u;
   };
   unsigned tp_ta = tp_tab_addr(1), tp_za = tp_row_addr(1);
+  // kTPS: this phase's P' and G as DPP broadcast sources (fmac_bcast), lane
+  // l holding entry l mod 16
+  double tabP = 0.0, tabG = 0.0;
+  auto tp_load_bcast = [&](int tb_) __attribute__((always_inline)) {
+    if constexpr (kTPS) {
+      const int sl = (lane & 15) < M ? (lane & 15) : 0;
+      const double* tb = ztab + tb_ * kTPh;
+      tabP = tb[sl];
+      tabG = tb[M + sl];
+    }
+  };
+  tp_load_bcast(1);
   unsigned tp_pa = (kTP && kPhiLds) ? lds_addr(phit + t) : 0u;
   (void)tp_ta;
   (void)tp_za;
@@ -1406,6 +1448,7 @@ fdcn_march(KArgs A) {
     if constexpr (kZLds) z_a = lds_addr(ztab + zoff_r);
     tp_ta = tp_tab_addr(0);
     tp_za = tp_row_addr(0);
+    tp_load_bcast(0);
   } else {
     ph = make_phase<kPair>(0.5, dt, ca, cc, cbc);
     setup_scan(ph);
@@ -1465,6 +1508,7 @@ fdcn_march(KArgs A) {
       if constexpr (kZLds) z_a = lds_addr(ztab + zoff_c);
       tp_ta = tp_tab_addr(1);
       tp_za = tp_row_addr(1);
+      tp_load_bcast(1);
     }
     // kSplit: the tabulated rhs terms; kPair: each scenario's from its own lanes
     double lo_new, hi_new;
@@ -1599,7 +1643,31 @@ fdcn_march(KArgs A) {
     if (shrt) V[NPT - 2] = 0.0;  // the phantom node's rhs
     }  // CN rhs
 
-    if constexpr (kTP) {
+    if constexpr (kTPS) {
+      // ---- 2. two-pass solve into T (zero-carry passes); Sherman-Morrison
+      // folded into the carries ------------------------------------------
+      solve_tp(ph);
+      const double g = smc_l * read_lane(cbv, 0);
+      tp_za = hide_addr(tp_za);
+      CC[0] = fma(g, lds_ld(tp_za, 0), CC[0]);
+      DD[0] = fma(g, lds_ld(tp_za, 1), DD[0]);
+      DD[0] = k2 * fma(CC[0], k1, DD[0]);  // short lanes (see setup_scan)
+      const double sC = ph.s * CC[0], sD = ph.s * DD[0];
+      // ---- 3. x = s (T + C P'_i + D G_i) - c2 V: c2 = 1 for theta = 1/2;
+      // the Rannacher steps (c2 = 0) drop V first
+      if (m < A.n_ranna) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) V[k] = 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < NPT; ++k)
+        asm volatile("v_fma_f64 %0, %1, %2, -%0" : "+v"(V[k]) : "s"(ph.s), "v"(T[k]));
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabP, sC, k);
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabG, sD, k);
+      if (shrt) V[NPT - 1] = 0.0;  // the phantom slot (its rhs must stay zero)
+    } else if constexpr (kTP) {
       // ---- 2. two-pass solve; Sherman-Morrison folded into the carries ----
       solve_tp(ph);
       const double g = smc_l * read_lane(cbv, 0);
