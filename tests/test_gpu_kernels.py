@@ -219,3 +219,25 @@ def test_large_batch_picks_paired_variant():
     # config-3 grids keep one scenario per wave (the paired flavour loses there)
     c3 = capi.plan(1024, False, B=10000)
     assert (c3["waves"], c3["npt"], c3["scen_per_block"]) == (1, 16, 1), c3
+
+
+@pytest.mark.parametrize("ko_lo", [-1, 20, 600], ids=["none", "inside_table", "covers_table"])
+def test_split_two_pass_every_step_knockout_vs_oracle(ko_lo, force_variant):
+    """Config-3 layout (CN split form on the two-pass solve, DPP-broadcast
+    tables, W=1 NPT=16) with a knock-out on every step, rebates on both sides,
+    accumulated tau on half the solves, both top-node layouts: the carried
+    boundary terms after a knock-out (ko_prev) and the folded
+    Sherman-Morrison correction under a projection that covers its lanes."""
+    force_variant(1, 16)
+    n_nodes, n_time = 1024, 150
+    rng = np.random.default_rng(1600 + ko_lo)
+    solves = []
+    for i in range(6):
+        s = random_solve(rng, n_nodes, n_time, 2, it=False, ko=False, drop_top=(i % 2 == 0))
+        s.ko_lo, s.ko_hi = ko_lo, (900 if i % 3 else 1 << 30)
+        s.mon_steps = list(range(1, n_time + 1)) if i < 3 else list(range(2, n_time + 1, 7))
+        s.mon_rebates = [0.0 if i % 2 else 1.25] * len(s.mon_steps)
+        s.tau_accumulate = i % 2 == 1
+        solves.append(s)
+    assert capi.variant_name(n_nodes, False, B=6) == "fdcn_march<0,1,16,0>"
+    _compare(solves, f"split two-pass every-step KO ko_lo={ko_lo}")
