@@ -384,11 +384,11 @@ __host__ __device__ constexpr int sub_chains(int it, int w, int npt, int zg) {
 // its update reads two tables per node against one, and at its 128-register
 // cap the prefetch spilled (10.9 ms against 5.5; 6.0 with S = 2 at three
 // waves per SIMD), so it keeps the re-run passes.
-// Round 3: the one-wave split-form CN variants up to 16 nodes per lane
-// (config 3) run two-pass too, with the homogeneous tables as DPP
+// Round 3: the one-wave split-form CN variants (up to 40 nodes per lane;
+// config 3: 16) run two-pass too, with the homogeneous tables as DPP
 // broadcasts (fmac_bcast) instead of the LDS reads that lost in round 2.
 __host__ __device__ constexpr bool two_pass(int it, int w, int npt, int zg) {
-  return w == 1 && zg == 0 && npt >= 2 && (it || npt <= 16);
+  return w == 1 && zg == 0 && npt >= 2 && (it || npt <= 40);
 }
 
 // Doubles of the correction tables per scenario.  Two-pass variants: per
@@ -732,7 +732,9 @@ fdcn_march(KArgs A) {
   // the split-form CN on the two-pass solve, tables as DPP broadcasts
   constexpr bool kTPS = kTP && !IT;
   static_assert(!kTP || (M >= 2 && !kPair), "two-pass: one scenario per wave, M >= 2");
-  static_assert(!kTPS || (kSplit && S == 1 && M <= 16), "split two-pass: S = 1, M <= 16");
+  static_assert(!kTPS || (kSplit && S == 1), "split two-pass: the split form, S = 1");
+  // DPP broadcast table registers per table (16 entries each)
+  constexpr int kTabRegs = kTPS ? (M + 15) / 16 : 1;
   const int kTPh = kTP ? 2 * M + lz * 2 * S : 0;  // doubles per phase
   // per sub-chain coefficients of the homogeneous part (two-pass solve), the
   // solution's value at the chunk's first node after the backward scan, and
@@ -1428,13 +1430,20 @@ fdcn_march(KArgs A) {
   unsigned tp_ta = tp_tab_addr(1), tp_za = tp_row_addr(1);
   // kTPS: this phase's P' and G as DPP broadcast sources (fmac_bcast), lane
   // l holding entry l mod 16
-  double tabP = 0.0, tabG = 0.0;
+  // (more than 16 slots: register r holds entries 16 r .. 16 r + 15)
+  double tabP[kTabRegs], tabG[kTabRegs];
+#pragma unroll
+  for (int r = 0; r < kTabRegs; ++r) tabP[r] = tabG[r] = 0.0;
   auto tp_load_bcast = [&](int tb_) __attribute__((always_inline)) {
     if constexpr (kTPS) {
-      const int sl = (lane & 15) < M ? (lane & 15) : 0;
       const double* tb = ztab + tb_ * kTPh;
-      tabP = tb[sl];
-      tabG = tb[M + sl];
+#pragma unroll
+      for (int r = 0; r < kTabRegs; ++r) {
+        const int e = 16 * r + (lane & 15);
+        const int sl = e < M ? e : 0;
+        tabP[r] = tb[sl];
+        tabG[r] = tb[M + sl];
+      }
     }
   };
   tp_load_bcast(1);
@@ -1663,9 +1672,9 @@ fdcn_march(KArgs A) {
       for (int k = 0; k < NPT; ++k)
         asm volatile("v_fma_f64 %0, %1, %2, -%0" : "+v"(V[k]) : "s"(ph.s), "v"(T[k]));
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabP, sC, k);
+      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabP[k / 16], sC, k % 16);
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabG, sD, k);
+      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabG[k / 16], sD, k % 16);
       if (shrt) V[NPT - 1] = 0.0;  // the phantom slot (its rhs must stay zero)
     } else if constexpr (kTP) {
       // ---- 2. two-pass solve; Sherman-Morrison folded into the carries ----
