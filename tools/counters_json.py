@@ -93,6 +93,8 @@ def main():
             "expected_read_bytes": exp_rd, "expected_write_bytes": exp_wr,
             "valu_insts_per_launch": sq["SQ_INSTS_VALU"],
             "valu_insts_per_node_step": sq["SQ_INSTS_VALU"] / node_steps,
+            # per lane: a wave instruction advances 64 lanes' chunks
+            "valu_insts_per_lane_node_step": 64.0 * sq["SQ_INSTS_VALU"] / node_steps,
             "valu_insts_per_wave": sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"],
             "f64_valu_insts_per_launch": f64,
             "fma_f64_per_launch": gr.get("SQ_INSTS_VALU_FMA_F64", 0.0),
@@ -108,7 +110,7 @@ def main():
                        f"--workload {wl} --steps 2 --warmup 1 (tools/pmc_counters.sh {tag})"),
         }
         print(f"{key}: HBM {(rd + wb) / 1e6:.1f} MB (expected {(exp_rd + exp_wr) / 1e6:.1f}), "
-              f"VALU/node-step {out[key]['valu_insts_per_node_step']:.2f}, "
+              f"VALU per lane node-step {out[key]['valu_insts_per_lane_node_step']:.2f}, "
               f"issue {out[key]['valu_issue_utilisation']:.2f} at {clk:.2f} GHz")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
