@@ -395,7 +395,7 @@ __host__ __device__ constexpr bool two_pass(int it, int w, int npt, int zg) {
 // phase P'[M], G[M], then [lz][C z(S), D z(S)]; otherwise z itself, [2][lz][NPT+1].
 __host__ __device__ constexpr int sm_doubles(int it, int w, int npt, int zg, int lz) {
   return two_pass(it, w, npt, zg)
-             ? 2 * (2 * (npt / sub_chains(it, w, npt, zg)) + lz * 2 * sub_chains(it, w, npt, zg))
+             ? 2 * (2 * (npt / sub_chains(it, w, npt, zg)) + (lz + 1) * 2 * sub_chains(it, w, npt, zg))
              : 2 * lz * (npt + 1);
 }
 
@@ -735,7 +735,9 @@ fdcn_march(KArgs A) {
   static_assert(!kTPS || (kSplit && S == 1), "split two-pass: the split form, S = 1");
   // DPP broadcast table registers per table (16 entries each)
   constexpr int kTabRegs = kTPS ? (M + 15) / 16 : 1;
-  const int kTPh = kTP ? 2 * M + lz * 2 * S : 0;  // doubles per phase
+  // doubles per phase: P', G, the lz Sherman-Morrison rows and a zero row
+  // (the lanes past the table read it)
+  const int kTPh = kTP ? 2 * M + (lz + 1) * 2 * S : 0;
   // per sub-chain coefficients of the homogeneous part (two-pass solve), the
   // solution's value at the chunk's first node after the backward scan, and
   // per-lane phase constants: P'_0 of the last sub-chain (short lanes: one
@@ -1175,6 +1177,19 @@ fdcn_march(KArgs A) {
   };
   (void)solve_tp;
 
+  // Two-pass: the Sherman-Morrison correction folded into one sub-chain's
+  // carries, C += y0 zc, D += y0 zd, with y0 the solution at interior node 0
+  // (cbv on lane 0) and (zc, zd) this lane's table row, already times the
+  // correction's coefficient (zero past the table).  y0 comes by v_readlane:
+  // a DPP row broadcast straight into the two FMAs (rows within the first 16
+  // lanes) measured slower (config 3 4.48 -> 4.52 ms, config 2 11.08 -> 11.87).
+  auto sm_fold = [&](double zc, double zd, double& c, double& d) __attribute__((always_inline)) {
+    const double y0 = read_lane(cbv, 0);
+    c = fma(y0, zc, c);
+    d = fma(y0, zd, d);
+  };
+  (void)sm_fold;
+
   // broadcast of the solution at interior node 0 (lane 0 of wave 0)
   auto bcast_first = [&](double v0lane) __attribute__((always_inline)) -> double {
     if constexpr (kPair) {  // lane 0 / lane 32: each scenario's own node 0
@@ -1214,19 +1229,23 @@ fdcn_march(KArgs A) {
         tph[lane] = acc;
         tph[M + lane] = pow_n<NPT>(p.bm, M - lane);
       }
-      if (t < lz) {
-        // z on every sub-chain of this lane is C_z P' + D_z G; on lane 0's
-        // first one the input e0/r itself contributes (1/r) P'
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-          tph[2 * M + t * 2 * S + j] = CC[j] + ((t == 0 && j == 0) ? p.inv_r : 0.0);
-          tph[2 * M + t * 2 * S + S + j] = DD[j];
-        }
-      }
       // z at interior node 0 (lane 0, slot 0: no forward carry there)
       const double d0 = (S == 1) ? k2 * fma(CC[0], k1, DD[0]) : DD[0];
       const double z0 = bcast_first(fma(d0, bmM, fma(CC[0], P0u, Out(0))));
-      return U(p.kappa / (1.0 + p.kappa * z0));
+      const double smc_p = U(p.kappa / (1.0 + p.kappa * z0));
+      if (t <= lz) {
+        // z on every sub-chain of this lane is C_z P' + D_z G; on lane 0's
+        // first one the input e0/r itself contributes (1/r) P'.  Stored times
+        // the correction's coefficient -smc, so a step adds y0 * row to its
+        // carries (y0: the solution at interior node 0); row lz is zero
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          const double c = CC[j] + ((t == 0 && j == 0) ? p.inv_r : 0.0);
+          tph[2 * M + t * 2 * S + j] = t < lz ? -smc_p * c : 0.0;
+          tph[2 * M + t * 2 * S + S + j] = t < lz ? -smc_p * DD[j] : 0.0;
+        }
+      }
+      return smc_p;
     }
     solve(p, std::false_type{});
     if (t < lz) {
@@ -1425,28 +1444,27 @@ fdcn_march(KArgs A) {
   // the Sherman-Morrison coefficients and of its payoff column (hide_addr)
   auto tp_tab_addr = [&](int tb_) { return kTP ? lds_addr(ztab + tb_ * kTPh) : 0u; };
   auto tp_row_addr = [&](int tb_) {
-    return kTP ? lds_addr(ztab + tb_ * kTPh + 2 * M + (t < lz ? t : lz - 1) * 2 * S) : 0u;
+    return kTP ? lds_addr(ztab + tb_ * kTPh + 2 * M + (t < lz ? t : lz) * 2 * S) : 0u;
   };
   unsigned tp_ta = tp_tab_addr(1), tp_za = tp_row_addr(1);
   // kTPS: this phase's P' and G as DPP broadcast sources (fmac_bcast), lane
-  // l holding entry l mod 16
-  // (more than 16 slots: register r holds entries 16 r .. 16 r + 15)
+  // l holding entry l mod 16 (more than 16 slots: register r holds entries
+  // 16 r .. 16 r + 15), times the phase's update scale s
   double tabP[kTabRegs], tabG[kTabRegs];
 #pragma unroll
   for (int r = 0; r < kTabRegs; ++r) tabP[r] = tabG[r] = 0.0;
-  auto tp_load_bcast = [&](int tb_) __attribute__((always_inline)) {
+  auto tp_load_bcast = [&](int tb_, double sc) __attribute__((always_inline)) {
     if constexpr (kTPS) {
       const double* tb = ztab + tb_ * kTPh;
 #pragma unroll
       for (int r = 0; r < kTabRegs; ++r) {
         const int e = 16 * r + (lane & 15);
         const int sl = e < M ? e : 0;
-        tabP[r] = tb[sl];
-        tabG[r] = tb[M + sl];
+        tabP[r] = sc * tb[sl];
+        tabG[r] = sc * tb[M + sl];
       }
     }
   };
-  tp_load_bcast(1);
   unsigned tp_pa = (kTP && kPhiLds) ? lds_addr(phit + t) : 0u;
   (void)tp_ta;
   (void)tp_za;
@@ -1457,11 +1475,12 @@ fdcn_march(KArgs A) {
     if constexpr (kZLds) z_a = lds_addr(ztab + zoff_r);
     tp_ta = tp_tab_addr(0);
     tp_za = tp_row_addr(0);
-    tp_load_bcast(0);
+    tp_load_bcast(0, ph.s);
   } else {
     ph = make_phase<kPair>(0.5, dt, ca, cc, cbc);
     setup_scan(ph);
     smc = smc_c;
+    tp_load_bcast(1, ph.s);
   }
   smc_l = sm_row * smc;
   s_l = shrt ? 0.0 : ph.s;
@@ -1517,7 +1536,7 @@ fdcn_march(KArgs A) {
       if constexpr (kZLds) z_a = lds_addr(ztab + zoff_c);
       tp_ta = tp_tab_addr(1);
       tp_za = tp_row_addr(1);
-      tp_load_bcast(1);
+      tp_load_bcast(1, ph.s);
     }
     // kSplit: the tabulated rhs terms; kPair: each scenario's from its own lanes
     double lo_new, hi_new;
@@ -1656,14 +1675,11 @@ fdcn_march(KArgs A) {
       // ---- 2. two-pass solve into T (zero-carry passes); Sherman-Morrison
       // folded into the carries ------------------------------------------
       solve_tp(ph);
-      const double g = smc_l * read_lane(cbv, 0);
       tp_za = hide_addr(tp_za);
-      CC[0] = fma(g, lds_ld(tp_za, 0), CC[0]);
-      DD[0] = fma(g, lds_ld(tp_za, 1), DD[0]);
+      sm_fold(lds_ld(tp_za, 0), lds_ld(tp_za, 1), CC[0], DD[0]);
       DD[0] = k2 * fma(CC[0], k1, DD[0]);  // short lanes (see setup_scan)
-      const double sC = ph.s * CC[0], sD = ph.s * DD[0];
-      // ---- 3. x = s (T + C P'_i + D G_i) - c2 V: c2 = 1 for theta = 1/2;
-      // the Rannacher steps (c2 = 0) drop V first
+      // ---- 3. x = s (T + C P'_i + D G_i) - c2 V (the tables carry s):
+      // c2 = 1 for theta = 1/2; the Rannacher steps (c2 = 0) drop V first
       if (m < A.n_ranna) {
 #pragma unroll
         for (int k = 0; k < NPT; ++k) V[k] = 0.0;
@@ -1672,21 +1688,17 @@ fdcn_march(KArgs A) {
       for (int k = 0; k < NPT; ++k)
         asm volatile("v_fma_f64 %0, %1, %2, -%0" : "+v"(V[k]) : "s"(ph.s), "v"(T[k]));
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabP[k / 16], sC, k % 16);
+      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabP[k / 16], CC[0], k % 16);
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabG[k / 16], sD, k % 16);
+      for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabG[k / 16], DD[0], k % 16);
       if (shrt) V[NPT - 1] = 0.0;  // the phantom slot (its rhs must stay zero)
     } else if constexpr (kTP) {
       // ---- 2. two-pass solve; Sherman-Morrison folded into the carries ----
       solve_tp(ph);
-      const double g = smc_l * read_lane(cbv, 0);
       tp_ta = hide_addr(tp_ta);  // this phase's tables
       tp_za = hide_addr(tp_za);
 #pragma unroll
-      for (int j = 0; j < S; ++j) {
-        CC[j] = fma(g, lds_ld(tp_za, j), CC[j]);
-        DD[j] = fma(g, lds_ld(tp_za, S + j), DD[j]);
-      }
+      for (int j = 0; j < S; ++j) sm_fold(lds_ld(tp_za, j), lds_ld(tp_za, S + j), CC[j], DD[j]);
       DD[S - 1] = k2 * fma(CC[S - 1], k1, DD[S - 1]);  // short lanes (see setup_scan)
       // ---- 3. x = Wr + C P'_i + D G_i and the step's update ---------------
       // nodes in (slot i, sub-chain j) order, four at a time: a slot's two

@@ -8,7 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$(mktemp -d)
 mkdir -p "$SRC/finite_difference_amd/csrc" "$SRC/include" "$ROOT/ab/$TAG"
 if [ "$REV" = "WT" ]; then
-  cp "$ROOT"/finite_difference_amd/csrc/*.hip "$SRC/finite_difference_amd/csrc/"
+  cp "$ROOT"/finite_difference_amd/csrc/*.hip "$ROOT"/finite_difference_amd/csrc/*.h "$SRC/finite_difference_amd/csrc/"
   cp "$ROOT"/include/*.h "$SRC/include/"
 else
   for f in $(git -C "$ROOT" ls-tree --name-only "$REV" finite_difference_amd/csrc/ include/); do
