@@ -877,6 +877,13 @@ fdcn_march(KArgs A) {
   // fz: std::true_type fuses the kRec update into the last backward pass
   auto solve = [&](const Phase& p, auto fz) __attribute__((always_inline)) {
     constexpr bool kFuse = decltype(fz)::value;
+    // one-wave variants: scan stages 0-1 run inline, the rest behind one
+    // uniform branch.  The recovery form keeps only stage 0 inline: config 5
+    // needs none at 64 nodes per lane (|fm|^63 < 1e-18), and stage 1 behind
+    // the branch took 17.50 -> 17.22 ms and 17.57 -> 17.25 in two A/B calls
+    // (stage 0 behind it as well: no better, 17.24).  The same move on the
+    // two-pass IT variant (config 2) cost 5 %: 10.68 -> 11.25 ms.
+    constexpr int kInlS = kRec ? 1 : 2;
     const double fm = p.fm, bm = p.bm;
     FDCN_PRIO_HI();  // pass 1 + scan raised, pass 2 at the base priority
     // forward pass 1: zero-carry end value of every sub-chain
@@ -902,20 +909,21 @@ fdcn_march(KArgs A) {
         // stages 0-1 inline, the rest behind one uniform branch.  The split
         // form tests stages 0-1 too (config 3 scenarios need one or two:
         // 5.17 -> 5.12 ms in A/B).  IT and the recovery form run them
-        // unconditionally: configs 2 and 5 need none (|fm|^(NPT-1) < 1e-18,
-        // the neighbour's aggregate is the whole carry), yet skipping them
+        // unconditionally (the recovery form stage 0 only, see kInlS):
+        // configs 2 and 5 need none (|fm|^(NPT-1) < 1e-18, the neighbour's
+        // aggregate is the whole carry), yet skipping both behind branches
         // measured no faster there (11.03 / 17.52 -> 11.03 / 17.65 ms), the
         // branches splitting the dependent chain the scheduler overlaps
-        if (j < 2 && (!kSplit || j < nst_f)) b = fma(FW[j], scan_up(b, d, lane4), b);
+        if (j < kInlS && (!kSplit || j < nst_f)) b = fma(FW[j], scan_up(b, d, lane4), b);
       } else if (j < nst_f) {
         b = fma(FW[j], scan_up(b, d, lane4), b);
       }
     }
-    if (W == 1 && nst_f > 2) {
+    if (W == 1 && nst_f > kInlS) {
 #pragma unroll
-      for (int j = 2; j < 6; ++j) {
+      for (int j = kInlS; j < 6; ++j) {
         const int d = 1 << j;
-        const double wf = kScanLds ? sw[(j - 2) * 128 + lane] : FW[j];
+        const double wf = (kScanLds && j >= 2) ? sw[(j - 2) * 128 + lane] : FW[j];
         if (j < nst_f) b = fma(wf, scan_up(b, d, lane4), b);
       }
     }
@@ -972,16 +980,16 @@ fdcn_march(KArgs A) {
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
       if constexpr (W == 1) {
-        if (j < 2 && (!kSplit || j < nst_b)) cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
+        if (j < kInlS && (!kSplit || j < nst_b)) cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
       } else if (j < nst_b) {
         cb = fma(GW[j], scan_dn(cb, d, lane4), cb);
       }
     }
-    if (W == 1 && nst_b > 2) {
+    if (W == 1 && nst_b > kInlS) {
 #pragma unroll
-      for (int j = 2; j < 6; ++j) {
+      for (int j = kInlS; j < 6; ++j) {
         const int d = 1 << j;
-        const double wg = kScanLds ? sw[(j - 2) * 128 + 64 + lane] : GW[j];
+        const double wg = (kScanLds && j >= 2) ? sw[(j - 2) * 128 + 64 + lane] : GW[j];
         if (j < nst_b) cb = fma(wg, scan_dn(cb, d, lane4), cb);
       }
     }
