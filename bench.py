@@ -767,13 +767,24 @@ def bench_trade(args):
     else:
         N, M = args.n_space or 4096, args.n_time or 8192
 
-        def trade():
+        def trade(window=True):
             d = FDDoubleBarrier(20.786, 21.0, 19.0, 23.0, 0.10994120968, "c", "out",
-                                n_space=N, n_time=M)
+                                n_space=N, n_time=M, active_window=window)
             return {"price": d.price(0.049493018, 0.0709454892, 49 / 365)}
         solves, node_steps = 1, N * M
         cfg = {"workload": f"trade_double_{N}x{M}", "config": "BASELINE configs[4]",
-               "facade": "FDDoubleBarrier.price(b, r, T), knock-out every step"}
+               "facade": "FDDoubleBarrier.price(b, r, T), knock-out every step; the "
+                         "façade marches the knock-out window (ko_window.py), "
+                         "full_grid_ms times active_window=False"}
+        from finite_difference_amd.ko_window import ko_window
+        _sv = FDDoubleBarrier(20.786, 21.0, 19.0, 23.0, 0.10994120968, "c", "out",
+                              n_space=N, n_time=M).solve_for(0.049493018, 0.0709454892, 49 / 365)
+        _w = ko_window(_sv, _sv.ko_value)
+        cfg["window_nodes"] = _w.solve.n_nodes if _w else None
+        cfg["grid_nodes"] = _sv.n_nodes
+        cfg["configured_node_steps"] = node_steps
+        if _w:  # node_steps_per_s counts the nodes the window marches
+            node_steps = _w.solve.n_nodes * M
 
     for _ in range(args.warmup):
         trade()
@@ -786,6 +797,14 @@ def bench_trade(args):
     times.sort()
     ms = sum(times) / len(times) * 1e3
     cfg["solves_per_trade"] = solves
+    if args.workload == "trade_double":  # the same trade on the whole grid
+        full = []
+        for _ in range(max(1, args.steps // 2)):
+            t0 = time.perf_counter()
+            rf = trade(window=False)
+            full.append(time.perf_counter() - t0)
+        cfg["full_grid_ms"] = sum(full) / len(full) * 1e3
+        cfg["full_grid_price"] = rf["price"]
     print(json.dumps({
         "metric": "single-trade latency through the drop-in facade",
         "value": ms, "unit": "ms/trade", "n_gpus": 1, "steps": args.steps,

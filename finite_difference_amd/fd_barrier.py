@@ -10,6 +10,12 @@ projection, discrete_barrier_fdm_pricer.py:413-440) -- or only at
 DoubleBarrier.price(b, r, T) (double _barrier.py:33), with both thresholds
 (the reference's "double-out" branch, :435-437), BASELINE config 5.
 
+With projection on every step (the default) the façades march only the
+live range between the barriers plus a decay margin (ko_window.py: the same
+values to 1e-18 relative, every node outside the window holding the
+projection value); ``active_window=False`` marches the whole grid.
+``solves()`` / ``solve_for()`` always return the whole-grid marches.
+
 Knock-ins use in/out parity with the closed-form vanilla, as the reference's
 pricers do (discrete_barrier_fdm_pricer.py:930-944).  Rebates follow
 BarrierEngine: out-rebates at hit (projection value K) or at expiry
@@ -25,7 +31,7 @@ from __future__ import annotations
 
 import bisect
 import math
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -34,6 +40,7 @@ from . import capi
 from .analytic import BarrierEngine, DoubleBarrier, _norm_rebate_timing, black_scholes
 from .barrier import tail_quantile
 from .engine import FORM_SUM, Boundary, Engine, Solve, default_engine, operator_coefficients
+from .ko_window import KoWindow, ko_window
 
 
 def _domain(cands: Sequence[float], sigma: float, T: float):
@@ -70,7 +77,7 @@ class FDBarrierEngine:
                  rebate_timing_out: Optional[str] = None, n_space: int = 1024,
                  n_time: int = 2000, rannacher_steps: int = 2,
                  monitor_times: Optional[Sequence[float]] = None,
-                 engine: Optional[Engine] = None):
+                 engine: Optional[Engine] = None, active_window: bool = True):
         # the analytic engine validates the flags and supplies the vanilla
         self.analytic = BarrierEngine(s, b, r, t, x, sigma, h, optionflag, directionflag,
                                       in_out_flag, k, barrier_status, rebate_timing_in,
@@ -84,6 +91,7 @@ class FDBarrierEngine:
         self.n_space, self.n_time, self.rannacher_steps = int(n_space), int(n_time), rannacher_steps
         self.monitor_times = monitor_times
         self.engine = engine
+        self.active_window = active_window
         self._value: Optional[float] = None
         self.s_nodes: List[float] = []
 
@@ -125,27 +133,36 @@ class FDBarrierEngine:
         def reb(tau):
             return out_reb if hit_now else out_reb * math.exp(-r * tau)
 
-        def ko(sv: Solve, value_fn) -> Solve:
+        def ko(sv: Solve, value_fn, value_bnd: Boundary) -> Solve:
             sv.ko_lo, sv.ko_hi = ko_lo, ko_hi
             sv.mon_steps = steps
             sv.mon_rebates = [value_fn(k * dt) for k in steps]
+            sv.ko_value = value_bnd  # the projection value as a function of tau (ko_window)
             return sv
 
         far = Boundary(FORM_SUM, out_reb, 0.0 if hit_now else -r, 0.0, 0.0)
         main = self._base(pay, lo if up else far, far if up else hi, dx)
-        out = [ko(main, reb)]
+        out = [ko(main, reb, far)]
         if self.in_out_flag == "i" and self.k != 0.0:
             K = self.k
             if self.rebate_timing_in == "expiry":   # K at expiry if never hit
                 v = np.full(n, K)
                 alive = Boundary(FORM_SUM, K, -r, 0.0, 0.0)
                 sv = self._base(v, alive if up else Boundary(), Boundary() if up else alive, dx)
-                out.append(ko(sv, lambda tau: 0.0))
+                out.append(ko(sv, lambda tau: 0.0, Boundary()))
             else:                                    # K at the first hit
                 v = np.zeros(n)
                 hitb = Boundary(FORM_SUM, K, 0.0, 0.0, 0.0)
                 sv = self._base(v, Boundary() if up else hitb, hitb if up else Boundary(), dx)
-                out.append(ko(sv, lambda tau: K))
+                out.append(ko(sv, lambda tau: K, hitb))
+        return out
+
+    def planned(self) -> List[Tuple[Solve, Optional[KoWindow]]]:
+        """The marches to launch: each of solves(), or its knock-out window."""
+        out = []
+        for sv in self.solves():
+            w = ko_window(sv, sv.ko_value) if self.active_window else None
+            out.append((w.solve if w else sv, w))
         return out
 
     def _interp(self, V: np.ndarray) -> float:
@@ -169,8 +186,9 @@ class FDBarrierEngine:
 
     def price(self) -> float:
         if self._value is None:
-            sv = self.solves()
-            self.finish(self._engine().run(sv) if sv else [])
+            plan = self.planned()
+            res = self._engine().run([p[0] for p in plan]) if plan else []
+            self.finish([w.expand(v) if w else v for (_, w), v in zip(plan, res)])
         return self._value
 
     def vanilla(self) -> float:
@@ -183,7 +201,7 @@ class FDDoubleBarrier:
     def __init__(self, S, X, L, U, sigma, callflag: str, inflag: str, m: int = 4,
                  n_space: int = 4096, n_time: int = 8192, rannacher_steps: int = 2,
                  monitor_times: Optional[Sequence[float]] = None,
-                 engine: Optional[Engine] = None):
+                 engine: Optional[Engine] = None, active_window: bool = True):
         self.S, self.X, self.L, self.U = float(S), float(X), float(L), float(U)
         self.sigma = float(sigma)
         self.callflag, self.inflag = callflag.lower(), inflag.lower()
@@ -195,6 +213,7 @@ class FDDoubleBarrier:
         self.n_space, self.n_time, self.rannacher_steps = int(n_space), int(n_time), rannacher_steps
         self.monitor_times = monitor_times
         self.engine = engine
+        self.active_window = active_window
         self.s_nodes: List[float] = []
 
     def solve_for(self, b: float, r: float, T: float) -> Solve:
@@ -215,6 +234,7 @@ class FDDoubleBarrier:
         sv.ko_hi = bisect.bisect_left(s, self.U)
         sv.mon_steps = _steps(self.n_time, T, self.monitor_times)
         sv.mon_rebates = [0.0] * len(sv.mon_steps)
+        sv.ko_value = Boundary()
         return sv
 
     def finish(self, V: np.ndarray, b: float, r: float, T: float) -> float:
@@ -234,16 +254,20 @@ class FDDoubleBarrier:
                 return out
             return float(black_scholes(self.callflag, self.S, self.X, r, b, self.sigma, T))
         eng = self.engine if self.engine is not None else default_engine()
-        V = eng.run([self.solve_for(b, r, T)])[0]
-        return self.finish(V, b, r, T)
+        sv = self.solve_for(b, r, T)
+        w = ko_window(sv, sv.ko_value) if self.active_window else None
+        V = eng.run([w.solve if w else sv])[0]
+        return self.finish(w.expand(V) if w else V, b, r, T)
 
 
 def price_many(engines: Sequence[FDBarrierEngine]) -> List[float]:
     """Price many FDBarrierEngine trades with their solves in shared launches."""
-    all_solves, spans = [], []
+    plans, spans, all_solves = [], [], []
     for e in engines:
-        sv = e.solves()
-        spans.append((len(all_solves), len(sv)))
-        all_solves.extend(sv)
+        plan = e.planned()
+        spans.append((len(all_solves), len(plan)))
+        plans.extend(plan)
+        all_solves.extend(p[0] for p in plan)
     res = engines[0]._engine().run(all_solves) if all_solves else []
+    res = [w.expand(v) if w else v for (_, w), v in zip(plans, res)]
     return [e.finish(res[a:a + n]) for e, (a, n) in zip(engines, spans)]

@@ -152,3 +152,35 @@ def test_config5_double_barrier_full_grid_vs_oracle():
     err = float(np.max(np.abs(Vg - Vo))) / max(1.0, float(np.max(np.abs(Vo))))
     print(f"[config5] rel err {err:.3e} price {d_gpu.finish(Vg, b, r, T)}")
     assert err <= 1e-10
+
+
+def test_config5_knockout_window_on_gpu_vs_whole_grid_oracle():
+    """The façade's default path (ko_window.py): the windowed march on the GPU
+    against the whole-grid oracle march, every node of the configured grid,
+    and the price through FDDoubleBarrier.price against the whole-grid
+    oracle price.  Single-barrier every-step engine too (one side cut)."""
+    from finite_difference_amd.fd_barrier import FDBarrierEngine
+    from finite_difference_amd.ko_window import ko_window
+    P = (20.786, 21.0, 19.0, 23.0, 0.10994120968)
+    b, r, T = 0.049493018, 0.0709454892, 49 / 365
+    d = FDDoubleBarrier(*P, "c", "out", n_space=4096, n_time=8192)
+    sv = d.solve_for(b, r, T)
+    w = ko_window(sv, sv.ko_value)
+    assert w is not None and w.solve.n_nodes < 0.2 * sv.n_nodes
+    Vg = w.expand(Engine().run([w.solve])[0])
+    Vo = oracle_engine().run([sv])[0]
+    err = float(np.max(np.abs(Vg - Vo))) / max(1.0, float(np.max(np.abs(Vo))))
+    print(f"[config5 window] {w.solve.n_nodes} of {sv.n_nodes} nodes, rel err {err:.3e}")
+    assert err <= 1e-10
+    p_gpu = FDDoubleBarrier(*P, "c", "out", n_space=4096, n_time=8192).price(b, r, T)
+    p_ref = FDDoubleBarrier(*P, "c", "out", n_space=4096, n_time=8192, engine=oracle_engine(),
+                            active_window=False).price(b, r, T)
+    assert abs(p_gpu - p_ref) <= 1e-10 + 1e-9 * abs(p_ref)
+    kw = dict(s=100.0, b=0.03, r=0.05, t=0.5, x=100.0, sigma=0.25, h=88.0, optionflag="p",
+              directionflag="d", in_out_flag="i", k=1.5, rebate_timing_in="hit",
+              n_space=2048, n_time=4000)
+    e_gpu = FDBarrierEngine(**kw)
+    assert all(wi is not None for _, wi in e_gpu.planned())
+    p_gpu = e_gpu.price()
+    p_ref = FDBarrierEngine(**kw, engine=oracle_engine(), active_window=False).price()
+    assert abs(p_gpu - p_ref) <= 1e-10 + 1e-9 * abs(p_ref)
