@@ -726,6 +726,8 @@ def bench_trade(args):
     from finite_difference_amd import capi, distributed
     if distributed.bind_device() is None:
         raise capi.FdcnError("no gfx950 device visible; the benchmark needs an MI355X")
+    if args.force_variant:  # A/B: every launch of the trade on that instance
+        capi.force_variant(*[int(x) for x in args.force_variant.split(",")])
     from finite_difference_amd import market
     from finite_difference_amd.american import AmericanFDMPricer, prefetch_many
     from finite_difference_amd.cn_log import DiscreteBarrierCrankNicolsonLog
