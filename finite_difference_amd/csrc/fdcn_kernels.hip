@@ -1716,6 +1716,17 @@ fdcn_march(KArgs A) {
       tp_pa = hide_addr(tp_pa);
       // node of the u-th entry of group q: slot (q+u)/S of sub-chain (q+u)%S
 #define FDCN_TP_K(u) ((((q) + (u)) % S) * M + ((q) + (u)) / S)
+      if constexpr (NPT % 4 != 0) {
+        // two-node chunks (the smallest grids): node by node, one sub-chain
+        static_assert(S == 1, "chunks of fewer than 4 nodes run one sub-chain");
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          V[k] = fma(DD[0], lds_ld(tp_ta, M + k), fma(CC[0], lds_ld(tp_ta, k), V[k]));
+          const double w = fma(ph.inv_r, V[k], -QS[k]);
+          V[k] = fmax(lds_ld(tp_pa, k * L), w);
+          QS[k] = fma(cq, V[k], -w);
+        }
+      } else {
       // the tables one group ahead of their use (LDS latency under the
       // previous group's arithmetic)
       double tpn[4], tgn[4];
@@ -1766,6 +1777,7 @@ fdcn_march(KArgs A) {
               "+v"(QS[FDCN_TP_K(2)]), "+v"(QS[FDCN_TP_K(3)])
             : "v"(pk[0]), "v"(pk[1]), "v"(pk[2]), "v"(pk[3]), "s"(ph.inv_r), "s"(cq));
       }
+      }  // NPT % 4 == 0
 #undef FDCN_TP_K
     } else {
     // ---- 2. tridiagonal solve ---------------------------------------------
@@ -2112,7 +2124,7 @@ Variant mk() {
 // nodes and small batches (latency).  W=16 workgroups are capped at 128
 // VGPRs (16 waves on one CU), so they use short chunks.
 #define FDCN_VARIANTS(IT)                                                                   \
-  mk<IT, 1, 4>(), mk<IT, 1, 8>(), mk<IT, 1, 12>(), mk<IT, 1, 16>(), mk<IT, 1, 24>(),        \
+  mk<IT, 1, 2>(), mk<IT, 1, 4>(), mk<IT, 1, 8>(), mk<IT, 1, 12>(), mk<IT, 1, 16>(), mk<IT, 1, 24>(),        \
       mk<IT, 1, 32>(), mk<IT, 1, 40>(), mk<IT, 1, 48>(), mk<IT, 1, 64>(), mk<IT, 2, 8>(),   \
       mk<IT, 2, 16>(),                                                                      \
       mk<IT, 2, 32>(), mk<IT, 2, 40>(), mk<IT, 4, 8>(), mk<IT, 4, 16>(), mk<IT, 4, 24>(),   \
@@ -2194,10 +2206,12 @@ const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
   // idle waves (a grid just above a variant's size) only when nothing else
   // fits, e.g. a large correction table that needs the LDS of a wider
   // variant; the table in the global workspace (ZG) only after that
-  for (int pass = 0; pass < 3 && !best; ++pass) {
+  // two-node chunks last of all: only the grids no other chunk length can lay
+  // out with at most one phantom slot per lane (5, 6 or 9 interior nodes)
+  for (int pass = 0; pass < 4 && !best; ++pass) {
     for (int i = 0; i < kNumVariants; ++i) {
       const Variant& v = kVariants[i];
-      if (v.it != it || v.lat || v.pair || v.zg != (pass == 2) ||
+      if (v.it != it || v.lat || v.pair || v.zg != (pass == 2) || (v.npt == 2) != (pass == 3) ||
           !fits(v, n_int, k_cap, pass == 0))
         continue;
       const long slots = (long)64 * v.w * v.npt;

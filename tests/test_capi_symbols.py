@@ -77,6 +77,20 @@ def test_plan_depends_on_batch_size():
     assert one["ws_bytes_per_scen"] > big["ws_bytes_per_scen"]
 
 
+def test_every_grid_from_five_nodes_has_a_variant():
+    """Every grid the ABI accepts (n_nodes >= 5) gets a kernel instance, at
+    batch sizes that reach the single-trade, throughput and paired choices.
+    (5, 7, 8 and 11 nodes had none before the two-node-chunk variants: no
+    chunk length of 4+ lays 3, 5, 6 or 9 interior nodes out with at most one
+    phantom slot per lane and the last lane full.)"""
+    for it in (False, True):
+        for n in range(5, 4200):
+            for B in (1, 4096):
+                p = capi.plan(n, it, B=B)
+                assert p["npt"] * 64 * p["waves"] >= n - 2, (n, it, B, p)
+    assert capi.plan(8, True, B=1)["npt"] == 2 and capi.plan(12, True, B=1)["npt"] == 4
+
+
 def test_invalid_size_reports_error():
     import pytest
     with pytest.raises(capi.FdcnError):

@@ -1,0 +1,80 @@
+"""Seeded random launches, HIP vs the CPU oracle, on the planner's own choice.
+
+The other kernel tests pin shapes and variants; these draw everything at
+once, per launch: CN or IT, grid size (6 to ~6000 nodes), step count,
+Rannacher steps (including n_ranna >= n_time), batch size (which moves the
+planner between the single-trade, throughput and paired flavours), and per
+scenario the boundary form, knock-out sides, monitoring schedule (sparse,
+or every step), rebates, accumulated tau and tau0.  Work per launch is
+bounded so the oracle finishes in well under a second.
+
+Bound: the kernel tests' 1e-10 of max(1, max|V|) per scenario, scaled by
+n/2048 above 2048 nodes (test_gpu_kernels.py explains the scaling).
+"""
+import numpy as np
+import pytest
+
+from finite_difference_amd import capi
+from finite_difference_amd.engine import Engine
+from plan_factory import random_solve
+from test_gpu_kernels import OracleBackend
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+WORK_CAP = 1.5e8  # node-steps per launch
+
+
+def _draw(seed: int):
+    rng = np.random.default_rng(9100 + seed)
+    it = bool(rng.integers(0, 2))
+    n_nodes = int(np.exp(rng.uniform(np.log(6), np.log(6000))))
+    n_time = int(rng.integers(1, 160))
+    n_ranna = int(rng.choice([0, 1, 2, 2, 3, 5]))
+    B = int(rng.choice([1, 2, 7, 33, 300, 1500]))
+    B = max(1, min(B, int(WORK_CAP // max(1, n_nodes * n_time))))
+    solves = []
+    for i in range(B):
+        s = random_solve(rng, n_nodes, n_time, n_ranna, it=it, drop_top=bool(rng.integers(0, 2)))
+        s.tau_accumulate = bool(rng.integers(0, 2))
+        s.tau0 = float(rng.choice([0.0, 0.0, 0.021]))
+        if not it and rng.integers(0, 4) == 0:  # every-step projection (config 5)
+            s.mon_steps = list(range(1, n_time + 1))
+            s.mon_rebates = [float(s.mon_rebates[0]) if len(s.mon_rebates) else 0.0] * n_time
+        solves.append(s)
+    return it, n_nodes, n_time, n_ranna, solves
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_random_launch_vs_oracle(seed):
+    it, n_nodes, n_time, n_ranna, solves = _draw(seed)
+    B = len(solves)
+    gpu = Engine().run(solves)
+    ref = Engine(OracleBackend()).run(solves)
+    tol = TOL * max(1.0, n_nodes / 2048)
+    worst = 0.0
+    for g, r in zip(gpu, ref):
+        assert np.all(np.isfinite(g))
+        worst = max(worst, float(np.max(np.abs(g - r))) / max(1.0, float(np.max(np.abs(r)))))
+    print(f"[fuzz {seed}] {'it' if it else 'cn'} n={n_nodes} m={n_time} r={n_ranna} B={B} "
+          f"{capi.variant_name(n_nodes, it, B=B)} worst={worst:.2e}")
+    assert worst <= tol
+
+
+def test_paired_flavour_random_batch_vs_oracle():
+    """A batch large enough for two scenarios per wave (B >= 4096, grids of
+    at most 2 * 64 * 4 nodes), mixed monitoring and odd B."""
+    rng = np.random.default_rng(9999)
+    n_nodes, n_time, B = 200, 40, 4097
+    solves = [random_solve(rng, n_nodes, n_time, 2, it=False, drop_top=bool(i % 2))
+              for i in range(B)]
+    for i, s in enumerate(solves):
+        s.tau_accumulate = i % 3 == 0
+    name = capi.variant_name(n_nodes, False, B=B)
+    assert name.endswith(",4>"), name  # the paired flavour (ZG bit 2)
+    gpu = Engine().run(solves)
+    ref = Engine(OracleBackend()).run(solves)
+    worst = max(float(np.max(np.abs(g - r))) / max(1.0, float(np.max(np.abs(r))))
+                for g, r in zip(gpu, ref))
+    print(f"[fuzz paired] {name} worst={worst:.2e}")
+    assert worst <= TOL

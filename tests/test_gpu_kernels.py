@@ -50,6 +50,7 @@ CASES = [
     (769, 120, 2), (1024, 150, 2), (1500, 90, 2), (2049, 128, 2), (2134, 60, 2),
     (2600, 40, 2), (3000, 30, 2), (4097, 24, 2), (4265, 20, 2), (9000, 12, 2),
     (300, 3, 5),
+    (5, 10, 2), (7, 30, 2), (8, 25, 0), (11, 40, 2),  # two-node chunks (NPT = 2)
 ]
 
 
@@ -78,7 +79,7 @@ def test_it_vs_oracle(n_nodes, n_time, n_ranna):
 # tau += dt) from a non-zero tau0.  The default choice depends on the batch
 # size, so small test batches alone would not reach the throughput variants
 # the bench uses.
-VARIANTS = [(1, 4, 0), (1, 8, 0), (1, 12, 0), (1, 16, 0), (1, 24, 0), (1, 32, 0), (1, 40, 0),
+VARIANTS = [(1, 2, 0), (1, 4, 0), (1, 8, 0), (1, 12, 0), (1, 16, 0), (1, 24, 0), (1, 32, 0), (1, 40, 0),
             (1, 48, 0), (1, 64, 0), (2, 8, 0), (2, 16, 0), (2, 32, 0), (2, 40, 0), (4, 8, 0), (4, 16, 0),
             (4, 24, 0), (4, 40, 0), (8, 8, 0), (8, 16, 0), (8, 40, 0), (16, 8, 0), (16, 24, 0),
             (16, 40, 0), (1, 8, 1), (1, 16, 1), (1, 32, 1)]
