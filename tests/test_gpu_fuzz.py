@@ -78,3 +78,38 @@ def test_paired_flavour_random_batch_vs_oracle():
                 for g, r in zip(gpu, ref))
     print(f"[fuzz paired] {name} worst={worst:.2e}")
     assert worst <= TOL
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_spot_space_pricer_vs_oracle(seed):
+    """fdcn_vc (the spot-space per-row CN of DiscreteBarrierFDMPricer2) on
+    seeded random trades: grid 6-3000 nodes, 5-200 steps, every barrier
+    type, weekly or no monitoring, the corrected explicit sign (the
+    reference's sign diverges, see test_spot_barrier.py)."""
+    import datetime as dt
+    from backends import oracle_engine
+    from finite_difference_amd.spot_barrier import DiscreteBarrierFDMPricer2
+    rng = np.random.default_rng(7300 + seed)
+    v0, v1 = dt.date(2025, 1, 6), dt.date(2025, 7, 7)
+    n = int(np.exp(rng.uniform(np.log(6), np.log(3000))))
+    m = int(rng.integers(5, 200))
+    bt = str(rng.choice(["none", "up-and-out", "down-and-out", "double-out", "up-and-in",
+                         "down-and-in"]))
+    S0 = 100.0
+    lo = float(rng.uniform(60.0, 95.0)) if ("down" in bt or "double" in bt) else None
+    hi = float(rng.uniform(105.0, 150.0)) if ("up" in bt or "double" in bt) else None
+    weekly = [v0 + dt.timedelta(days=7 * i) for i in range(1, 26)] if rng.integers(0, 2) else None
+    p = DiscreteBarrierFDMPricer2(
+        spot=S0, strike=float(rng.uniform(80.0, 120.0)), valuation_date=v0, maturity_date=v1,
+        volatility=float(rng.uniform(0.12, 0.45)), option_type=str(rng.choice(["call", "put"])),
+        barrier_type=bt, lower_barrier=lo, upper_barrier=hi, monitoring_dates=weekly,
+        flat_rate_nacc=float(rng.uniform(0.0, 0.08)), num_space_nodes=n, num_time_steps=m,
+        engine=Engine(), explicit_sign="corrected")
+    _, _, solves = p._grid_solves()
+    gpu = Engine().run_vc(solves)
+    ref = oracle_engine().run_vc(solves)
+    worst = max(float(np.max(np.abs(g - r))) / max(1.0, float(np.max(np.abs(r))))
+                for g, r in zip(gpu, ref))
+    print(f"[fuzz vc {seed}] n={n} m={m} {bt} monitored={weekly is not None} "
+          f"solves={len(solves)} worst={worst:.2e}")
+    assert worst <= TOL * max(1.0, n / 2048)
