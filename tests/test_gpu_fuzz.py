@@ -113,3 +113,44 @@ def test_random_spot_space_pricer_vs_oracle(seed):
     print(f"[fuzz vc {seed}] n={n} m={m} {bt} monitored={weekly is not None} "
           f"solves={len(solves)} worst={worst:.2e}")
     assert worst <= TOL * max(1.0, n / 2048)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_american_trade_device_vs_oracle(seed):
+    """The whole American stack on seeded random trades: the device path
+    (session marches per dividend segment, spline jumps and the Richardson /
+    cubic Greeks epilogue on the GPU) against the host path on the CPU oracle
+    (oracle march, host jumps, host epilogue).  Put or call, 0-2 cash
+    dividends, 40-400 space nodes and steps.  Bounds: price and vega 1e-9,
+    delta / gamma / theta 1e-7 relative to max(1, |x|) (the device epilogue
+    solves the 4x4 cubic with its own LU, not LAPACK's)."""
+    import datetime as dt
+    from backends import oracle_engine
+    from finite_difference_amd import market
+    from finite_difference_amd.american import AmericanFDMPricer
+    rng = np.random.default_rng(8800 + seed)
+    val, mat = dt.date(2025, 7, 28), dt.date(2025, 7, 28) + dt.timedelta(days=int(rng.integers(20, 300)))
+    n_div = int(rng.integers(0, 3))
+    span = (mat - val).days
+    divs = sorted((val + dt.timedelta(days=int(d)), float(rng.uniform(0.2, 2.5)))
+                  for d in rng.choice(np.arange(1, span), size=n_div, replace=False))
+    naca = float(rng.uniform(0.0, 0.09))
+    kw = dict(spot=float(rng.uniform(60.0, 140.0)), strike=100.0, valuation_date=val,
+              maturity_date=mat, sigma=float(rng.uniform(0.12, 0.5)),
+              option_type=str(rng.choice(["put", "call"])), dividend_schedule=divs,
+              num_space_nodes=int(rng.integers(40, 400)), num_time_steps=int(rng.integers(40, 400)),
+              rannacher_steps=int(rng.choice([0, 2])))
+
+    def make(engine):
+        curve = market.iso_curve(market.create_rate_df(naca))
+        return AmericanFDMPricer(discount_curve=curve, forward_curve=curve, engine=engine, **kw)
+
+    dev, host = make(Engine()), make(oracle_engine())
+    pd_, ph = dev.price_log2(), host.price_log2()
+    gd, gh = dev.greeks_log2(), host.greeks_log2()
+    print(f"[fuzz american {seed}] {kw['option_type']} N={kw['num_space_nodes']} "
+          f"M={kw['num_time_steps']} divs={n_div} price {pd_:.6f} vs {ph:.6f}")
+    assert abs(pd_ - ph) <= 1e-9 * max(1.0, abs(ph))
+    for k, tol in (("price", 1e-9), ("vega", 1e-9), ("delta", 1e-7), ("gamma", 1e-7),
+                   ("theta", 1e-7)):
+        assert abs(gd[k] - gh[k]) <= tol * max(1.0, abs(gh[k])), (k, gd[k], gh[k])
