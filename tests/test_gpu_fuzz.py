@@ -154,3 +154,45 @@ def test_random_american_trade_device_vs_oracle(seed):
     for k, tol in (("price", 1e-9), ("vega", 1e-9), ("delta", 1e-7), ("gamma", 1e-7),
                    ("theta", 1e-7)):
         assert abs(gd[k] - gh[k]) <= tol * max(1.0, abs(gh[k])), (k, gd[k], gh[k])
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_barrier_trade_device_vs_oracle(seed):
+    """DiscreteBarrierFDMPricer (the runner's pricer) on seeded random trades:
+    every barrier type, call/put, parity-mode or explicit grids, rebates at
+    hit or at expiry, one-sided Greeks near the barrier, dividends; the
+    device path (one launch, Greeks epilogue on the GPU) against the host
+    path on the CPU oracle.  price_log2 and every greeks_log2 key to 1e-9 of
+    max(1, |x|) (the march differs by rounding; the epilogue is the same
+    arithmetic)."""
+    import datetime as dt
+    from backends import oracle_engine
+    from finite_difference_amd import scenarios
+    rng = np.random.default_rng(6600 + seed)
+    val = dt.date(2025, 7, 28)
+    mat = val + dt.timedelta(days=int(rng.integers(10, 200)))
+    S0 = 100.0
+    bt = str(rng.choice(["up-and-out", "down-and-out", "up-and-in", "down-and-in"]))
+    up = float(rng.uniform(103.0, 150.0)) if "up" in bt else None
+    lo = float(rng.uniform(60.0, 97.0)) if "down" in bt else None
+    mon = sorted({val + dt.timedelta(days=int(d)) for d in rng.integers(1, (mat - val).days + 1,
+                                                                         int(rng.integers(1, 30)))})
+    divs = ([(val + dt.timedelta(days=int(rng.integers(1, (mat - val).days))), 0.8)]
+            if rng.integers(0, 3) == 0 else [])
+    kw = dict(opt_type=str(rng.choice(["call", "put"])), divs=divs,
+              rebate_amount=float(rng.choice([0.0, 0.0, 1.25])),
+              rebate_at_hit=bool(rng.integers(0, 2)),
+              use_one_sided_greeks_near_barrier=bool(rng.integers(0, 2)),
+              num_space_nodes=int(rng.integers(60, 600)), num_time_steps=int(rng.integers(50, 500)),
+              grid_mode=str(rng.choice(["parity", "explicit"])))
+    args = (S0, float(rng.uniform(80.0, 120.0)), float(rng.uniform(0.12, 0.45)),
+            float(rng.uniform(0.0, 0.09)), bt, up, lo, val, mat, mon)
+    dev = scenarios.make_barrier_pricer(*args, engine=Engine(), **kw)
+    host = scenarios.make_barrier_pricer(*args, engine=oracle_engine(), **kw)
+    pd_, ph = dev.price_log2(), host.price_log2()
+    gd, gh = dev.greeks_log2(), host.greeks_log2()
+    print(f"[fuzz barrier {seed}] {bt} {kw['opt_type']} {kw['grid_mode']} "
+          f"N={kw['num_space_nodes']} M={kw['num_time_steps']} price {pd_:.6f} vs {ph:.6f}")
+    assert abs(pd_ - ph) <= 1e-9 * max(1.0, abs(ph))
+    for k in gh:
+        assert abs(gd[k] - gh[k]) <= 1e-9 * max(1.0, abs(gh[k])), (k, gd[k], gh[k])
