@@ -11,6 +11,8 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 \
     --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
+# the driver's smoke check (__graft_entry__.smoke, no build: the tree's .so)
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py > $O/bench_american.json 2> $O/bench_american.err || exit $?
 for wl in barrier double analytic scenario_file american_file trade_cnlog trade_american trade_double; do
   timeout -k 10 300 python bench.py --workload $wl > $O/bench_$wl.json 2> $O/bench_$wl.err || exit $?
