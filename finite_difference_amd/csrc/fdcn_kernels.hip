@@ -731,6 +731,9 @@ fdcn_march(KArgs A) {
   constexpr bool kTP = two_pass(IT, W, NPT, ZG);
   // the split-form CN on the two-pass solve, tables as DPP broadcasts
   constexpr bool kTPS = kTP && !IT;
+  // kTPS: the homogeneous part added to T before the update (tables not
+  // scaled by s), the phantom slot zeroed by its scale instead of a reset
+  constexpr bool kTPST = kTPS && NPT <= 16;
   static_assert(!kTP || (M >= 2 && !kPair), "two-pass: one scenario per wave, M >= 2");
   static_assert(!kTPS || (kSplit && S == 1), "split two-pass: the split form, S = 1");
   // DPP broadcast table registers per table (16 entries each)
@@ -1474,6 +1477,8 @@ fdcn_march(KArgs A) {
     }
   };
   unsigned tp_pa = (kTP && kPhiLds) ? lds_addr(phit + t) : 0u;
+  // kTPS tables: times the update scale s, or unscaled for kTPST
+  auto tab_scale = [&]() __attribute__((always_inline)) { return kTPST ? 1.0 : ph.s; };
   (void)tp_ta;
   (void)tp_za;
   (void)tp_pa;
@@ -1483,12 +1488,12 @@ fdcn_march(KArgs A) {
     if constexpr (kZLds) z_a = lds_addr(ztab + zoff_r);
     tp_ta = tp_tab_addr(0);
     tp_za = tp_row_addr(0);
-    tp_load_bcast(0, ph.s);
+    tp_load_bcast(0, tab_scale());
   } else {
     ph = make_phase<kPair>(0.5, dt, ca, cc, cbc);
     setup_scan(ph);
     smc = smc_c;
-    tp_load_bcast(1, ph.s);
+    tp_load_bcast(1, tab_scale());
   }
   smc_l = sm_row * smc;
   s_l = shrt ? 0.0 : ph.s;
@@ -1544,7 +1549,7 @@ fdcn_march(KArgs A) {
       if constexpr (kZLds) z_a = lds_addr(ztab + zoff_c);
       tp_ta = tp_tab_addr(1);
       tp_za = tp_row_addr(1);
-      tp_load_bcast(1, ph.s);
+      tp_load_bcast(1, tab_scale());
     }
     // kSplit: the tabulated rhs terms; kPair: each scenario's from its own lanes
     double lo_new, hi_new;
@@ -1688,6 +1693,23 @@ fdcn_march(KArgs A) {
       DD[0] = k2 * fma(CC[0], k1, DD[0]);  // short lanes (see setup_scan)
       // ---- 3. x = s (T + C P'_i + D G_i) - c2 V (the tables carry s):
       // c2 = 1 for theta = 1/2; the Rannacher steps (c2 = 0) drop V first
+      if constexpr (kTPST) {
+        // the homogeneous part into T (unscaled tables), then x = s T - c2 V
+        // with the phantom slot's scale s_l = 0 on short lanes: its V stays
+        // an exact zero without a reset
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) fmac_bcast(T[k], tabP[k / 16], CC[0], k % 16);
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) fmac_bcast(T[k], tabG[k / 16], DD[0], k % 16);
+        if (m < A.n_ranna) {
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) V[k] = 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < NPT - 1; ++k)
+          asm volatile("v_fma_f64 %0, %1, %2, -%0" : "+v"(V[k]) : "s"(ph.s), "v"(T[k]));
+        asm volatile("v_fma_f64 %0, %1, %2, -%0" : "+v"(V[NPT - 1]) : "v"(s_l), "v"(T[NPT - 1]));
+      } else {
       if (m < A.n_ranna) {
 #pragma unroll
         for (int k = 0; k < NPT; ++k) V[k] = 0.0;
@@ -1700,6 +1722,7 @@ fdcn_march(KArgs A) {
 #pragma unroll
       for (int k = 0; k < NPT; ++k) fmac_bcast(V[k], tabG[k / 16], DD[0], k % 16);
       if (shrt) V[NPT - 1] = 0.0;  // the phantom slot (its rhs must stay zero)
+      }
     } else if constexpr (kTP) {
       // ---- 2. two-pass solve; Sherman-Morrison folded into the carries ----
       solve_tp(ph);
