@@ -1691,8 +1691,11 @@ fdcn_march(KArgs A) {
       tp_za = hide_addr(tp_za);
       sm_fold(lds_ld(tp_za, 0), lds_ld(tp_za, 1), CC[0], DD[0]);
       DD[0] = k2 * fma(CC[0], k1, DD[0]);  // short lanes (see setup_scan)
-      // ---- 3. x = s (T + C P'_i + D G_i) - c2 V (the tables carry s):
-      // c2 = 1 for theta = 1/2; the Rannacher steps (c2 = 0) drop V first
+      // ---- 3. x = s (T + C P'_i + D G_i) - c2 V: c2 = 1 for theta = 1/2;
+      // the Rannacher steps (c2 = 0) drop V first.  Up to 16 nodes per lane
+      // (kTPST) the tables go into T first; longer chunks (2-3 table
+      // registers) keep tables pre-scaled by s, added to V after the update
+      // (A/B: kTPST lost 1.3 % at 40 nodes per lane, won 0.5-3.6 % at 8-16)
       if constexpr (kTPST) {
         // the homogeneous part into T (unscaled tables), then x = s T - c2 V
         // with the phantom slot's scale s_l = 0 on short lanes: its V stays
