@@ -88,3 +88,26 @@ def test_cpu_cores_record():
     assert 1 <= n <= rec["affinity_cpus"]
     if rec["cgroup_cpu_quota"]:
         assert n <= rec["cgroup_cpu_quota"]
+
+
+def test_parity_record_flags_a_wrong_launch():
+    """cpu_baseline's parity record on CPU: the oracle's own outputs pass, a
+    result off by 1e-8 of the scale in one node of one scenario fails, and a
+    NaN is reported as not finite (bench.py exits 3 on either)."""
+    import numpy as np
+    import bench
+    from oracle import oracle
+    g = bench.build_barrier(6, 64, 40, seed=0)
+    ref = oracle.cn_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams, g.v_init,
+                          g.mon_step, g.mon_rebate, 1)
+    _, par = bench.cpu_baseline(g, 0.01, ref.copy())
+    assert par["ok"] and par["all_finite"] and par["max_rel_err"] == 0.0
+    n = par["n_compared"]
+    bad = ref.copy()
+    bad[n - 1, g.n_nodes // 2] += 1e-8 * max(1.0, float(np.max(np.abs(ref[n - 1]))))
+    _, par = bench.cpu_baseline(g, 0.01, bad)
+    assert not par["ok"] and par["max_rel_err"] > bench.PARITY_TOL
+    nan = ref.copy()
+    nan[0, 3] = np.nan
+    _, par = bench.cpu_baseline(g, 0.01, nan)
+    assert not par["all_finite"]
