@@ -25,9 +25,10 @@
  *     node 0 (S_min side), node n_nodes-1 (S_max side), interior 1..n_nodes-2.
  *     The production barrier engine's top-node drop (…pricer.py:449,543) is
  *     expressed by the caller passing n_nodes = N_s and v_init = payoff[0:N_s];
- *     the kernel has no quirk flag.  Any n_nodes >= 5 is accepted (grids
- *     whose interior does not fill a wavefront are padded with inactive
- *     lanes; 5-11-node grids run two nodes per lane).
+ *     the kernel has no quirk flag.  5 <= n_nodes <= 40962 (16 wavefronts
+ *     x 64 lanes x 40 nodes + 2) is accepted: grids whose interior does not
+ *     fill the lanes are padded with inactive lanes, 5-11-node grids run two
+ *     nodes per lane; larger grids fail with FDCN_EINVAL.
  *   - Step m = 0..n_time-1 advances tau to tau_m = tau0 + (m+1)*dt and uses
  *     theta = 1 for m < n_ranna (Rannacher), 0.5 afterwards.
  *   - All arrays are C-contiguous, row-major, fp64 / int32.  The caller owns

@@ -89,6 +89,12 @@ def test_every_grid_from_five_nodes_has_a_variant():
                 p = capi.plan(n, it, B=B)
                 assert p["npt"] * 64 * p["waves"] >= n - 2, (n, it, B, p)
     assert capi.plan(8, True, B=1)["npt"] == 2 and capi.plan(12, True, B=1)["npt"] == 4
+    # up to the largest layout (16 waves x 64 lanes x 40 nodes + 2), and no further
+    for n in list(range(4200, 40963, 97)) + [40962]:
+        p = capi.plan(n, n % 2 == 0, B=1)
+        assert p["npt"] * 64 * p["waves"] >= n - 2, (n, p)
+    with pytest.raises(capi.FdcnError):
+        capi.plan(40963, False, B=1)
 
 
 def test_invalid_size_reports_error():
