@@ -196,3 +196,65 @@ def test_random_barrier_trade_device_vs_oracle(seed):
     assert abs(pd_ - ph) <= 1e-9 * max(1.0, abs(ph))
     for k in gh:
         assert abs(gd[k] - gh[k]) <= 1e-9 * max(1.0, abs(gh[k])), (k, gd[k], gh[k])
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_cn_log_trade_device_vs_oracle(seed):
+    """DiscreteBarrierCrankNicolsonLog (config 1's class) on seeded random
+    trades: barrier side and in/out, rebate, a random monitoring set, auto
+    grids; device (three sigma solves in one launch, device epilogue) against
+    the host path on the oracle, price and every Greek to 1e-9 of max(1, |x|)."""
+    from backends import oracle_engine
+    from finite_difference_amd.cn_log import DiscreteBarrierCrankNicolsonLog
+    rng = np.random.default_rng(5500 + seed)
+    T = float(rng.uniform(0.05, 0.8))
+    bt = str(rng.choice(["up-and-out", "down-and-out", "up-and-in", "down-and-in"]))
+    kw = dict(S0=100.0, K=float(rng.uniform(80.0, 120.0)), T=T, sigma=float(rng.uniform(0.12, 0.45)),
+              r_disc=float(rng.uniform(0.0, 0.08)), b_carry=float(rng.uniform(-0.02, 0.08)),
+              option_type=str(rng.choice(["call", "put"])), barrier_type=bt,
+              lower_barrier=float(rng.uniform(60.0, 95.0)) if "down" in bt else None,
+              upper_barrier=float(rng.uniform(105.0, 150.0)) if "up" in bt else None,
+              rebate=float(rng.choice([0.0, 0.0, 1.0])),
+              monitor_times=sorted(float(x) for x in rng.uniform(0.0, T, int(rng.integers(1, 20)))),
+              N_space=int(rng.integers(64, 700)), N_time=int(rng.integers(50, 900)))
+    dev = DiscreteBarrierCrankNicolsonLog(**kw, engine=Engine())
+    host = DiscreteBarrierCrankNicolsonLog(**kw, engine=oracle_engine())
+    pd_, ph = dev.price(), host.price()
+    print(f"[fuzz cn_log {seed}] {bt} {kw['option_type']} N={kw['N_space']} M={kw['N_time']} "
+          f"price {pd_:.6f} vs {ph:.6f}")
+    assert abs(pd_ - ph) <= 1e-9 * max(1.0, abs(ph))
+    gd, gh = dev.greeks(), host.greeks()
+    for k in gh:
+        assert abs(gd[k] - gh[k]) <= 1e-9 * max(1.0, abs(gh[k])), (k, gd[k], gh[k])
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_black76_american_device_vs_oracle(seed):
+    """AmericanFwdFDMPricer (Black-76 on the forward, the IT kernel with the
+    forward's coefficients) on seeded random trades, device vs the host path
+    on the oracle: price_log2 and greeks_log2 (Δ/Γ/θ 1e-7, the rest 1e-9)."""
+    import datetime as dt
+    from backends import oracle_engine
+    from finite_difference_amd import market
+    from finite_difference_amd.american_black76 import AmericanFwdFDMPricer
+    rng = np.random.default_rng(4400 + seed)
+    val = dt.date(2025, 7, 28)
+    kw = dict(spot=float(rng.uniform(60.0, 140.0)), strike=100.0, valuation_date=val,
+              maturity_date=val + dt.timedelta(days=int(rng.integers(20, 300))),
+              sigma=float(rng.uniform(0.12, 0.5)), option_type=str(rng.choice(["put", "call"])),
+              num_space_nodes=int(rng.integers(40, 400)), num_time_steps=int(rng.integers(40, 400)),
+              rannacher_steps=2)
+    naca = float(rng.uniform(0.0, 0.09))
+
+    def make(engine):
+        curve = market.iso_curve(market.create_rate_df(naca))
+        return AmericanFwdFDMPricer(discount_curve=curve, forward_curve=curve, engine=engine, **kw)
+
+    dev, host = make(Engine()), make(oracle_engine())
+    pd_, ph = dev.price_log2(), host.price_log2()
+    gd, gh = dev.greeks_log2(), host.greeks_log2()
+    print(f"[fuzz black76 {seed}] {kw['option_type']} price {pd_:.6f} vs {ph:.6f}")
+    assert abs(pd_ - ph) <= 1e-9 * max(1.0, abs(ph))
+    for k in gh:
+        tol = 1e-7 if k in ("delta", "gamma", "theta") else 1e-9
+        assert abs(gd[k] - gh[k]) <= tol * max(1.0, abs(gh[k])), (k, gd[k], gh[k])
