@@ -258,3 +258,45 @@ def test_random_black76_american_device_vs_oracle(seed):
     for k in gh:
         tol = 1e-7 if k in ("delta", "gamma", "theta") else 1e-9
         assert abs(gd[k] - gh[k]) <= tol * max(1.0, abs(gh[k])), (k, gd[k], gh[k])
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_analytic_pricer_device_vs_oracle(seed):
+    """DiscreteBarrierFDMPricerAnalytic on seeded random trades (corrected
+    explicit sign): every barrier type, monthly / weekly / daily monitoring
+    (daily takes the FIS continuous-window decision: BGK closed forms through
+    the batched GPU engines, or the every-step CN overlay), rebates and their
+    timing, the Douady double-barrier engine on or off; the device path
+    against the host path on the oracle, price to 1e-9 and Greeks to 1e-7 of
+    max(1, |x|)."""
+    import pandas as pd
+    from backends import oracle_engine
+    from finite_difference_amd import market
+    from finite_difference_amd.spot_barrier_analytic import DiscreteBarrierFDMPricerAnalytic
+    rng = np.random.default_rng(3300 + seed)
+    val, mat = pd.Timestamp("2025-07-28"), pd.Timestamp("2026-01-28")
+    step = int(rng.choice([1, 7, 30]))
+    mon = [val + pd.Timedelta(days=d) for d in range(step, (mat - val).days + 1, step)]
+    bt = str(rng.choice(["up-and-out", "down-and-out", "up-and-in", "down-and-in", "double-out",
+                         "double-in", "none"]))
+    c = market.create_rate_df(float(rng.uniform(0.0, 0.08)))
+    c["Date"] = pd.to_datetime(c["Date"], format="%Y/%m/%d").dt.strftime("%Y-%m-%d")
+    kw = dict(trade_id="T1", direction=str(rng.choice(["long", "short"])), quantity=1,
+              contract_multiplier=1.0, valuation_date=val, maturity_date=mat, discount_curve=c,
+              forward_curve=c, dividend_schedule=[], monitoring_dates=mon,
+              double_barrier_analytic=bool(rng.integers(0, 2)), spot=100.0,
+              strike=float(rng.uniform(85.0, 115.0)), volatility=float(rng.uniform(0.15, 0.4)),
+              option_type=str(rng.choice(["call", "put"])), barrier_type=bt,
+              lower_barrier=float(rng.uniform(65.0, 92.0)) if ("down" in bt or "double" in bt) else None,
+              upper_barrier=float(rng.uniform(108.0, 140.0)) if ("up" in bt or "double" in bt) else None,
+              rebate_amount=float(rng.choice([0.0, 0.0, 1.0])),
+              space_nodes=int(rng.integers(120, 500)), time_steps=int(rng.integers(20, 300)),
+              explicit_sign="corrected")
+    dev = DiscreteBarrierFDMPricerAnalytic(**kw, engine=Engine())
+    host = DiscreteBarrierFDMPricerAnalytic(**kw, engine=oracle_engine())
+    pg, ph = dev.price(), host.price()
+    print(f"[fuzz analytic {seed}] {bt} every {step}d {kw['option_type']} price {pg:.6f} vs {ph:.6f}")
+    assert abs(pg - ph) <= 1e-9 * max(1.0, abs(ph))
+    gg, gh = dev.greeks(), host.greeks()
+    for k in gh:
+        assert abs(gg[k] - gh[k]) <= 1e-7 * max(1.0, abs(gh[k])), (k, gg[k], gh[k])
