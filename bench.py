@@ -265,6 +265,53 @@ def host_cores():
                "omp_max_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
+# scenarios per rank in the sampled parity record of multi-GPU runs
+PARITY_SAMPLE = 8
+
+
+def sample_parity(group, res, k: int) -> dict:
+    """The parity record of the first k scenarios of `res` (this rank's timed
+    output) against the C oracle, every node (cpu_baseline's rule)."""
+    import numpy as np
+    from oracle import oracle
+    k = min(k, group.B)
+    nthreads, _ = host_cores()
+    sl = slice(0, k)
+    if group.it:
+        ref = oracle.it_batch(group.n_nodes, group.n_time, group.n_ranna, group.params[sl],
+                              group.iparams[sl], group.v_init[sl], group.payoff[sl], nthreads)
+    else:
+        ref = oracle.cn_batch(group.n_nodes, group.n_time, group.n_ranna, group.params[sl],
+                              group.iparams[sl], group.v_init[sl], group.mon_step,
+                              group.mon_rebate, nthreads)
+    got = np.asarray(res[:k])
+    scale = np.maximum(1.0, np.max(np.abs(ref), axis=1))
+    rel = np.max(np.abs(got - ref), axis=1) / scale
+    rel = np.where(np.isnan(rel), np.inf, rel)  # a NaN must not vanish in the MAX reduction
+    return {"max_rel_err": float(np.max(rel)) if rel.size else 0.0, "n_compared": int(k),
+            "nodes_per_scenario": int(group.n_nodes), "tol": PARITY_TOL,
+            "ok": bool(np.all(rel <= PARITY_TOL)), "all_finite": bool(np.all(np.isfinite(got))),
+            "rule": "per scenario max_j |V_gpu - V_oracle| / max(1, max_j |V_oracle|), every "
+                    "node of the timed launch's output vs the C oracle (oracle/fdcn_oracle.c)"}
+
+
+def reduce_parity(part: dict, world: int, device) -> dict:
+    """Every rank's sample_parity record -> the job's: the worst error and
+    finiteness over the ranks (MAX), the compared scenarios summed."""
+    import torch
+    import torch.distributed as dist
+    worst = torch.tensor([part["max_rel_err"], 0.0 if part["all_finite"] else 1.0],
+                         dtype=torch.float64, device=device)
+    cnt = torch.tensor([float(part["n_compared"])], dtype=torch.float64, device=device)
+    dist.all_reduce(worst, op=dist.ReduceOp.MAX)
+    dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    err = float(worst[0].item())
+    return dict(part, max_rel_err=err, all_finite=not worst[1].item() > 0,
+                n_compared=int(cnt.item()), ok=bool(err <= PARITY_TOL),
+                rule=part["rule"] + f"; the first {PARITY_SAMPLE} scenarios of every rank's "
+                                    f"shard, worst over the {world} ranks")
+
+
 def cpu_baseline(group, seconds: float, res=None):
     """Two variants of the reference algorithm, each on a
     bounded sample of the same batch:
@@ -500,6 +547,10 @@ def run_rank(args):
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(g, args.cpu_seconds, res)
+    elif world > 1 and not args.no_cpu_baseline:
+        # every rank checks a sample of its own timed output against the C
+        # oracle on its host cores; the record is the worst over the ranks
+        parity = reduce_parity(sample_parity(g, res, PARITY_SAMPLE), world, dev)
 
     if rank == 0:
         config = {"workload": workload, "scenarios_per_gpu": g.B, "grid": [n_space, n_time],

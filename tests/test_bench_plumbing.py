@@ -111,3 +111,80 @@ def test_parity_record_flags_a_wrong_launch():
     nan[0, 3] = np.nan
     _, par = bench.cpu_baseline(g, 0.01, nan)
     assert not par["all_finite"]
+
+
+def test_sample_parity_record_of_a_rank():
+    """sample_parity (the per-rank record of multi-GPU bench runs): the
+    oracle's own outputs pass, one node off by 1e-8 of the scale fails, and a
+    NaN turns into an infinite error (so it survives the MAX over ranks) and
+    a non-finite flag; both the American and the barrier groups."""
+    import numpy as np
+    import bench
+    from oracle import oracle
+    for g in (bench.build_barrier(5, 64, 40, seed=1), bench.build_american(5, 64, 40, seed=1)):
+        k = 3
+        if g.it:
+            ref = oracle.it_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams, g.v_init,
+                                  g.payoff, 1)
+        else:
+            ref = oracle.cn_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams, g.v_init,
+                                  g.mon_step, g.mon_rebate, 1)
+        par = bench.sample_parity(g, ref.copy(), k)
+        assert par["ok"] and par["all_finite"] and par["max_rel_err"] == 0.0
+        assert par["n_compared"] == k
+        bad = ref.copy()
+        bad[k - 1, g.n_nodes // 2] += 1e-8 * max(1.0, float(np.max(np.abs(ref[k - 1]))))
+        par = bench.sample_parity(g, bad, k)
+        assert not par["ok"] and par["max_rel_err"] > bench.PARITY_TOL
+        bad[k, 0] = np.nan  # outside the sample: not seen
+        assert not bench.sample_parity(g, bad, k)["ok"]
+        nan = ref.copy()
+        nan[1, 3] = np.nan
+        par = bench.sample_parity(g, nan, k)
+        assert not par["all_finite"] and par["max_rel_err"] == float("inf") and not par["ok"]
+        assert bench.sample_parity(g, ref, 99)["n_compared"] == g.B
+
+
+def _parity_rank(rank, world, port, out_path):
+    """One gloo rank of test_reduce_parity_over_two_ranks: rank 1's sample
+    carries a wrong node (the barrier group of bench.py, seed = rank)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    import torch.distributed as dist
+    import bench
+    from oracle import oracle
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        g = bench.build_barrier(4, 64, 40, seed=rank)
+        res = oracle.cn_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams, g.v_init,
+                              g.mon_step, g.mon_rebate, 1)
+        good = bench.reduce_parity(bench.sample_parity(g, res, 2), world, "cpu")
+        if rank == 1:
+            res[1, 7] += 1e-6 * max(1.0, abs(res[1]).max())
+        bad = bench.reduce_parity(bench.sample_parity(g, res, 2), world, "cpu")
+        with open(f"{out_path}.{rank}", "w") as f:
+            json.dump([good, bad], f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reduce_parity_over_two_ranks(tmp_path):
+    """The multi-GPU bench's parity record (reduce_parity over gloo): the
+    worst error over the ranks and the compared scenarios summed, the same on
+    every rank, so a wrong node on rank 1 fails rank 0's line too."""
+    import torch.multiprocessing as mp
+    import bench
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "par")
+    mp.start_processes(_parity_rank, args=(2, port, out), nprocs=2, join=True,
+                       start_method="spawn")
+    recs = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    for good, bad in recs:
+        assert good["ok"] and good["max_rel_err"] == 0.0 and good["n_compared"] == 4
+        assert not bad["ok"] and bad["max_rel_err"] > bench.PARITY_TOL and bad["n_compared"] == 4
+        assert "worst over the 2 ranks" in bad["rule"]
+    assert recs[0][1] == recs[1][1]
