@@ -77,7 +77,8 @@ N_SIMD = 1024
 # with the factorisation hoisted 5, IT update 5)
 BYTES_PER_NODE_STEP = {True: 32, False: 16}   # IT: V and lambda in+out; CN: V in+out
 FLOPS_PER_NODE_STEP = {True: 17, False: 10}
-DEFAULT_BATCH = {"american": 4096, "barrier": 10000, "double": 2048, "analytic": 1 << 20}
+DEFAULT_BATCH = {"american": 4096, "barrier": 10000, "double": 2048, "analytic": 1 << 20,
+                 "spot_vc": 4096}
 TRADE_WORKLOADS = ("trade_cnlog", "trade_american", "trade_double", "scenario_file",
                    "american_file")
 KERNEL_SRC = os.path.join(ROOT, "finite_difference_amd", "csrc", "fdcn_kernels.hip")
@@ -431,6 +432,8 @@ def spawn_ranks(args, argv) -> int:
 def run_rank(args):
     if args.workload == "analytic":
         return bench_analytic(args)
+    if args.workload == "spot_vc":
+        return bench_spot_vc(args)
     if args.workload == "scenario_file":
         return bench_scenario_file(args)
     if args.workload == "american_file":
@@ -868,6 +871,154 @@ def bench_trade(args):
         "node_steps_per_s": node_steps / (ms * 1e-3), "result": res}), flush=True)
 
 
+def build_spot_vc(B: int, n_space: int, n_time: int, seed: int = 0):
+    """SURVEY §8(f)3 workload: B DiscreteBarrierFDMPricer2 trades (uniform S
+    grid, per-row CN coefficients, FIS barrier rows; discrete_barrier_fdm_
+    pricer_2.py:336-428) over a strike / vol / barrier sweep, up / down /
+    double knock-out, call and put, daily monitoring over one year.  The
+    explicit terms take the corrected sign (the reference's own sign makes
+    the march diverge, tests/test_spot_barrier.py).  One march per trade."""
+    import numpy as np
+    from finite_difference_amd.engine import pack_vc
+    from finite_difference_amd.spot_barrier import DiscreteBarrierFDMPricer2
+    rng = np.random.default_rng(20250106 + seed)
+    v0, v1 = dt.date(2025, 1, 6), dt.date(2026, 1, 6)
+    daily = [v0 + dt.timedelta(days=i) for i in range(1, (v1 - v0).days + 1)]
+    kinds = ["up-and-out", "down-and-out", "double-out"]
+    solves = []
+    for i in range(B):
+        bt = kinds[i % 3]
+        lo = float(rng.uniform(60.0, 92.0)) if bt != "up-and-out" else None
+        hi = float(rng.uniform(108.0, 150.0)) if bt != "down-and-out" else None
+        p = DiscreteBarrierFDMPricer2(
+            spot=100.0, strike=float(rng.uniform(80.0, 120.0)), valuation_date=v0,
+            maturity_date=v1, volatility=float(rng.uniform(0.15, 0.45)),
+            option_type=("call", "put")[(i // 3) % 2], barrier_type=bt, lower_barrier=lo,
+            upper_barrier=hi, monitoring_dates=daily, flat_rate_nacc=0.05,
+            num_space_nodes=n_space, num_time_steps=n_time, explicit_sign="corrected")
+        solves.extend(p._grid_solves()[2])
+    return pack_vc(solves, list(range(len(solves))))
+
+
+def vc_cpu_baseline(group, seconds: float, res=None):
+    """The C oracle's spot-space march (oracle_vc_batch: the reference's
+    per-step Thomas, discrete_barrier_fdm_pricer_2.py:336-428) on a bounded
+    sample of the same batch, OpenMP over scenarios on the host cores, and
+    the parity record of the GPU outputs `res` of those scenarios."""
+    import numpy as np
+    from oracle import oracle
+    nthreads, cores_rec = host_cores()
+    done, t_total, m, parts = 0, 0.0, nthreads, []
+    while t_total < seconds and done < group.B:
+        m = min(m, group.B - done)
+        sl = slice(done, done + m)
+        t0 = time.perf_counter()
+        parts.append(oracle.vc_batch(group.n_nodes, group.n_time, group.n_ranna, group.diag[sl],
+                                     group.bnd[sl], group.v_init[sl], group.iparams[sl],
+                                     group.mon_step, group.mon_rebate, nthreads))
+        t_total += time.perf_counter() - t0
+        done += m
+        m *= 2
+    units = group.n_nodes - 1
+    cpu = {"value": done * units * group.n_time / t_total, "unit": "node-steps/s",
+           "cores": nthreads, "kind": "port",
+           "sample": f"{done} of the {group.B} scenarios, full {units}x{group.n_time} grid, "
+                     f"{t_total:.1f} s; C oracle (oracle_vc_batch, per-step Thomas of "
+                     f"discrete_barrier_fdm_pricer_2.py:336-428), OpenMP over scenarios on "
+                     f"{_cpu_model()}", **cores_rec}
+    parity = None
+    if res is not None:
+        ref = np.concatenate(parts)
+        got = np.asarray(res[:done])
+        scale = np.maximum(1.0, np.max(np.abs(ref), axis=1))
+        rel = np.max(np.abs(got - ref), axis=1) / scale
+        rel = np.where(np.isnan(rel), np.inf, rel)
+        parity = {"max_rel_err": float(np.max(rel)), "n_compared": int(done),
+                  "nodes_per_scenario": int(group.n_nodes), "tol": PARITY_TOL,
+                  "ok": bool(np.all(rel <= PARITY_TOL)),
+                  "all_finite": bool(np.all(np.isfinite(got))),
+                  "rule": "per scenario max_j |V_gpu - V_oracle| / max(1, max_j |V_oracle|), "
+                          "every node of the timed launch's output vs the C oracle"}
+    return cpu, parity
+
+
+def bench_spot_vc(args):
+    """the spot-space per-row CN march (fdcn_vc_batch_dev) of
+    B Pricer2 trades, node-steps/s, with the fp64-VALU roofline, the C
+    oracle's CPU rate and the parity record of the timed output."""
+    import numpy as np
+    import torch
+    from finite_difference_amd import capi, distributed
+    capi.require_device()
+    dev = torch.device("cuda", distributed.bind_device())
+    n_space, n_time = args.n_space or 1024, args.n_time or 2000
+    B = args.batch or DEFAULT_BATCH["spot_vc"]
+    t_build = time.perf_counter()
+    g = build_spot_vc(B, n_space, n_time)
+    t_build = time.perf_counter() - t_build
+    plan = capi.vc_plan(g.n_nodes, B=g.B)
+    ws_bytes = max(8, plan["ws_bytes_per_scen"] * g.B)
+    D, Bd = torch.from_numpy(g.diag).to(dev), torch.from_numpy(g.bnd).to(dev)
+    V0, I = torch.from_numpy(g.v_init).to(dev), torch.from_numpy(g.iparams).to(dev)
+    MS = torch.from_numpy(g.mon_step if len(g.mon_step) else np.zeros(1, np.int32)).to(dev)
+    MR = torch.from_numpy(g.mon_rebate if len(g.mon_rebate) else np.zeros(1)).to(dev)
+    out = torch.empty_like(V0)
+    ws = torch.empty(ws_bytes // 8, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        capi.vc_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, D.data_ptr(), Bd.data_ptr(),
+                          V0.data_ptr(), I.data_ptr(), len(g.mon_step), MS.data_ptr(),
+                          MR.data_ptr(), out.data_ptr(), ws.data_ptr(), ws_bytes,
+                          stream.cuda_stream)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
+    res = out.cpu().numpy()
+    cpu = parity = None
+    if not args.no_cpu_baseline:
+        cpu, parity = vc_cpu_baseline(g, args.cpu_seconds, res)
+    units = g.n_nodes - 1
+    node_steps = g.B * units * g.n_time
+    fps = FLOPS_PER_NODE_STEP[False]
+    tf = fps * node_steps / (kernel_ms * 1e-3) / 1e12
+    gbs = BYTES_PER_NODE_STEP[False] * node_steps / (kernel_ms * 1e-3) / 1e9
+    slots = 64 * plan["waves"] * plan["npt"]
+    print(json.dumps({
+        "metric": "spot-space CN grid-node-steps/sec/GPU (DiscreteBarrierFDMPricer2 march)",
+        "value": node_steps * args.steps / elapsed, "unit": "node-steps/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (strike/vol/barrier sweep of Pricer2 knock-outs, daily monitoring)",
+        "config": {"workload": f"spot_vc_{n_space}x{n_time}_batch{g.B}", "scenarios": g.B,
+                   "grid": [n_space, n_time], "n_nodes": g.n_nodes, "rannacher_steps": 2,
+                   "explicit_sign": "corrected"},
+        "roofline": {"bound": "fp64_valu", "achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": tf / FP64_VALU_PEAK_TFLOPS, "traffic": None,
+                     "flops_per_node_step": fps},
+        "roofline_hbm_effective": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "bytes_per_node_step": BYTES_PER_NODE_STEP[False]},
+        "kernel_ms_per_launch": kernel_ms,
+        "kernel": {"name": f"fdcn_vc_march<{plan['waves']},{plan['npt']}>", **plan,
+                   "slots": slots, "slot_use": g.n_nodes / slots},
+        "outputs_finite": bool(np.all(np.isfinite(res))), "parity": parity,
+        "host_build_s": t_build, "cpu_baseline": cpu}), flush=True)
+    if parity is not None and not (parity["ok"] and parity["all_finite"]):
+        print(f"bench.py: PARITY FAILURE {parity}", file=sys.stderr, flush=True)
+        return 3
+    return 0
+
+
 def bench_analytic(args):
     """Closed-form barrier batch (fdcn_rr_barrier_batch_dev): contracts/s."""
     import numpy as np
@@ -952,7 +1103,7 @@ def main(argv=None):
         from finite_difference_amd import capi
         capi.LIB_PATH = os.path.abspath(args.lib)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        if args.workload in TRADE_WORKLOADS or args.workload == "analytic":
+        if args.workload in TRADE_WORKLOADS or args.workload in ("analytic", "spot_vc"):
             raise SystemExit(f"--workload {args.workload} is a single-GPU measurement")
         return spawn_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -377,6 +377,16 @@ def vc_batch(n_nodes: int, n_time: int, n_ranna: int, diag, bnd, v_init, iparams
     return out
 
 
+def vc_batch_dev(B: int, n_nodes: int, n_time: int, n_ranna: int, diag_ptr: int, bnd_ptr: int,
+                 v_init_ptr: int, iparams_ptr: int, n_mon: int, mon_step_ptr: int,
+                 mon_rebate_ptr: int, v_out_ptr: int, workspace_ptr: int, workspace_bytes: int,
+                 stream_ptr: int) -> None:
+    """fdcn_vc_batch_dev: every array already on the device (bench, sessions)."""
+    _check(lib().fdcn_vc_batch_dev(B, n_nodes, n_time, n_ranna, diag_ptr, bnd_ptr, v_init_ptr,
+                                   iparams_ptr, n_mon, mon_step_ptr, mon_rebate_ptr, v_out_ptr,
+                                   workspace_ptr, workspace_bytes, stream_ptr))
+
+
 def vc_plan(n_nodes: int, *, B: int) -> dict:
     w, npt = ctypes.c_int32(), ctypes.c_int32()
     ws = ctypes.c_int64()

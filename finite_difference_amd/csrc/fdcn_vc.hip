@@ -23,7 +23,11 @@
 // and passes through the lower padding and node 0 (multiplier 1, rhs 0);
 // the top value g_{n-1} hi enters as the backward carry-in at the last slot
 // and passes through the upper padding and node n-1.  So neither boundary
-// needs a per-slot select.
+// needs a per-slot select.  A grid one node longer than the slots (the
+// reference's N + 1 nodes on N = 64 W NPT, e.g. 1 025 nodes in 1 024
+// slots) keeps node 0 out of the slots (pad_lo = -1): its value is the
+// forward carry-in g_0 lo itself, held as one uniform scalar that feeds the
+// stencil of node 1 on the next step (bitwise what the slot would hold).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -130,6 +134,8 @@ __device__ void factor_phase(const double* P, int n, int slots, int pad_lo, doub
     const double beta = (i == 0) ? mn[0] : mn[i] - sub[i] * cs;
     const double g = 1.0 / beta;
     cs = (i < n - 1) ? sup[i] / beta : 0.0;
+    if (i == 0) scal[0] = g;
+    if (s < 0) continue;  // node 0 outside the slots (pad_lo = -1)
     const bool interior = i > 0 && i < n - 1;
     cA[s] = interior ? ae[i] * g : 0.0;
     cB[s] = interior ? be[i] * g : 0.0;
@@ -138,7 +144,6 @@ __device__ void factor_phase(const double* P, int n, int slots, int pad_lo, doub
     // backward one (g_{n-1} hi); interior rows their factors
     cf[s] = (i == 0) ? 1.0 : (i == n - 1 ? 0.0 : -sub[i] * g);
     cE[s] = (i == n - 1) ? 1.0 : (i == 0 ? 0.0 : -cs);
-    if (i == 0) scal[0] = g;
     if (i == n - 1) scal[1] = g;
   }
   for (int s = pad_lo + n; s < slots; ++s) {  // upper padding: pass the backward carry down
@@ -181,6 +186,10 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
 
   double V[NPT], R[NPT];
   const double* vin = A.v_init + (size_t)scen * n;
+  // node 0 outside the slots: its value (uniform), and whether it knocks out
+  const bool lo_out = pad_lo < 0;
+  double v0 = lo_out ? uni(vin[0]) : 0.0;
+  const bool ko0 = 0 <= ko_lo || 0 >= ko_hi;
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     const int j = base + k - pad_lo;
@@ -189,6 +198,12 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
 
   double cA[NPT], cB[NPT], cC[NPT], cf[NPT], ce[NPT];
   double FW[6], GW[6], Fpre = 0.0, Gsuf = 0.0, g0 = 0.0, gN = 0.0;
+  // the zero-carry passes run as two half-chunk chains joined by the
+  // multiplier product of the other half (upper half forward, lower half
+  // backward): half the dependent FMA chain on a one-wave-per-SIMD kernel
+  constexpr bool kHalf = NPT >= 8;
+  constexpr int H = NPT / 2;
+  double fh = 1.0, gl = 1.0;
   auto load_phase = [&](int ph) __attribute__((always_inline)) {
     if constexpr (W > 1) __syncthreads();  // previous readers of the wave totals are done
     const double* C = coef + (size_t)ph * kNC * slots;
@@ -207,6 +222,14 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
     for (int k = 0; k < NPT; ++k) {
       f *= cf[k];
       g *= ce[k];
+    }
+    if constexpr (kHalf) {
+      fh = 1.0;
+      gl = 1.0;
+#pragma unroll
+      for (int k = H; k < NPT; ++k) fh *= cf[k];
+#pragma unroll
+      for (int k = 0; k < H; ++k) gl *= ce[k];
     }
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -244,6 +267,7 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
 
     // ---- rhs: the reference's explicit stencil, pre-scaled by g_i ---------
     double left = from_below(V[NPT - 1], 1, lane4), right = from_above(V[0], 1, lane4);
+    if (lo_out && t == 0) left = v0;
     if constexpr (W > 1) {
       if (lane == 63) xch[wave] = V[NPT - 1];
       if (lane == 0) xch[W + wave] = V[0];
@@ -260,8 +284,18 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
 
     // ---- forward: d_i = rhs'_i + f_i d_{i-1}; carry-in at slot 0: g_0 lo ----
     double a = 0.0;
+    if constexpr (kHalf) {
+      double al = 0.0, ah = 0.0;
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) a = fma(cf[k], a, R[k]);
+      for (int k = 0; k < H; ++k) {
+        al = fma(cf[k], al, R[k]);
+        ah = fma(cf[k + H], ah, R[k + H]);
+      }
+      a = fma(fh, al, ah);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) a = fma(cf[k], a, R[k]);
+    }
 #pragma unroll
     for (int j = 0; j < 6; ++j) a = fma(FW[j], from_below(a, 1 << j, lane4), a);
     double cw = g0 * lo;  // carry into wave 0
@@ -277,6 +311,7 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
     }
     double c = from_below(a, 1, lane4);
     if (lane == 0) c = cw;
+    if (lo_out) v0 = uni(g0 * lo);  // x_0 of this step: cw of wave 0
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       c = fma(cf[k], c, R[k]);
@@ -285,8 +320,18 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
 
     // ---- backward: x_i = d_i + e_i x_{i+1}; carry-in at the top: g_{n-1} hi --
     double b = 0.0;
+    if constexpr (kHalf) {
+      double bl = 0.0, bh = 0.0;
 #pragma unroll
-    for (int k = NPT - 1; k >= 0; --k) b = fma(ce[k], b, R[k]);
+      for (int k = H - 1; k >= 0; --k) {
+        bh = fma(ce[k + H], bh, R[k + H]);
+        bl = fma(ce[k], bl, R[k]);
+      }
+      b = fma(gl, bh, bl);
+    } else {
+#pragma unroll
+      for (int k = NPT - 1; k >= 0; --k) b = fma(ce[k], b, R[k]);
+    }
 #pragma unroll
     for (int j = 0; j < 6; ++j) b = fma(GW[j], from_above(b, 1 << j, lane4), b);
     double cwb = gN * hi;  // carry into the last wave
@@ -321,6 +366,7 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
                      : "v"(rlo), "v"(rhi), "s"(km[k]));
         V[k] = __longlong_as_double(((long long)hi32 << 32) | lo32);
       }
+      if (lo_out && ko0) v0 = reb;
       ++mpos;
       while (mpos < mend && __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) <= m + 1) ++mpos;
       next_mon = mpos < mend ? __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) : 0x7fffffff;
@@ -334,6 +380,7 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
     const int j = base + k - pad_lo;
     if (j >= 0 && j < n) vout[j] = V[k];
   }
+  if (lo_out && t == 0) vout[0] = v0;
 }
 
 using VcFn = void (*)(VcArgs);
@@ -345,8 +392,11 @@ template <int W, int NPT>
 VcVariant vmk() {
   return VcVariant{W, NPT, &fdcn_vc_march<W, NPT>};
 }
-const VcVariant kVc[] = {vmk<1, 4>(),  vmk<1, 8>(),  vmk<1, 16>(), vmk<4, 4>(), vmk<4, 8>(),
-                         vmk<4, 16>(), vmk<16, 4>(), vmk<16, 8>(), vmk<16, 16>()};
+// (W = 16 holds at most 128 VGPRs a wave and spills its NPT = 8 and 16
+// bodies; W = 8 keeps 256 and serves grids up to 8 193 nodes without)
+const VcVariant kVc[] = {vmk<1, 4>(),  vmk<1, 8>(),  vmk<1, 16>(), vmk<4, 4>(),
+                         vmk<4, 8>(),  vmk<4, 16>(), vmk<8, 8>(),  vmk<8, 16>(),
+                         vmk<16, 4>(), vmk<16, 8>(), vmk<16, 16>()};
 constexpr int kNumVc = sizeof(kVc) / sizeof(kVc[0]);
 
 // Throughput batches: fewest waves, then fewest slots.  Small batches (B
@@ -356,7 +406,7 @@ const VcVariant* vc_choose(int n, long B) {
   const bool small = B * 4 < 2048;
   for (int i = 0; i < kNumVc; ++i) {
     const VcVariant& v = kVc[i];
-    if (64L * v.w * v.npt < n) continue;
+    if (64L * v.w * v.npt < n - 1) continue;  // node 0 may sit outside (pad_lo = -1)
     if (!best) {
       best = &v;
       continue;
@@ -397,7 +447,7 @@ int vc_launch(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna, const
   a.n_time = n_time;
   a.n_ranna = n_ranna;
   a.slots = 64 * v->w * v->npt;
-  a.pad_lo = (a.slots - n_nodes) / 2;
+  a.pad_lo = a.slots >= n_nodes ? (a.slots - n_nodes) / 2 : -1;
   a.diag = diag;
   a.bnd = bnd;
   a.v_init = v_init;

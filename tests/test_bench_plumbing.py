@@ -188,3 +188,28 @@ def test_reduce_parity_over_two_ranks(tmp_path):
         assert not bad["ok"] and bad["max_rel_err"] > bench.PARITY_TOL and bad["n_compared"] == 4
         assert "worst over the 2 ranks" in bad["rule"]
     assert recs[0][1] == recs[1][1]
+
+
+def test_spot_vc_workload_and_parity_record():
+    """bench.py --workload spot_vc on CPU: the Pricer2 batch packs one march
+    per trade with its knock-out lanes and daily monitoring, the device plan
+    accepts it, and vc_cpu_baseline's parity record passes the oracle's own
+    outputs and fails a wrong node."""
+    import numpy as np
+    import bench
+    from finite_difference_amd import capi
+    from oracle import oracle
+    g = bench.build_spot_vc(6, 64, 40)  # Pricer2 takes N = max(200, num_space_nodes)
+    assert g.B == 6 and g.n_nodes == 201 and g.n_time == 40 and g.n_ranna == 2
+    assert g.diag.shape == (6, 2, 6, 201)
+    assert len(g.mon_step) > 0 and np.all(g.iparams[:, capi.I_MON_COUNT] > 0)
+    assert capi.vc_plan(g.n_nodes, B=g.B)["waves"] >= 1
+    ref = oracle.vc_batch(g.n_nodes, g.n_time, g.n_ranna, g.diag, g.bnd, g.v_init, g.iparams,
+                          g.mon_step, g.mon_rebate, 1)
+    assert np.all(np.isfinite(ref))
+    cpu, par = bench.vc_cpu_baseline(g, 0.01, ref.copy())
+    assert par["ok"] and par["max_rel_err"] == 0.0 and cpu["value"] > 0
+    bad = ref.copy()
+    bad[0, 30] += 1e-6 * max(1.0, np.abs(ref[0]).max())
+    _, par = bench.vc_cpu_baseline(g, 0.01, bad)
+    assert not par["ok"]

@@ -131,3 +131,32 @@ def test_spot_price_on_gpu_matches_black_scholes():
     p = make(inp, Engine(), explicit_sign="corrected")
     ref = _bs(100.0, 100.0, 0.05, 0.25, p.tenor_years, True)
     assert abs(p.price() - ref) < 1e-2 * ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [257, 513, 1024, 1025, 1026, 2049, 4097, 4098, 8193])
+@pytest.mark.parametrize("B", [1, 600])
+def test_spot_kernel_grid_one_node_longer_than_the_slots(n, B):
+    """N + 1 nodes on N = 64 W NPT slots (1 025 = the reference's 1 024-step
+    grid): node 0 stays outside the slots as a scalar (fdcn_vc pad_lo = -1).
+    A down-and-out knocks node 0 out on every weekly date, so the scalar's
+    projection is covered; n = slots and slots + 2 keep the padded layout."""
+    from finite_difference_amd import capi
+    weekly = [(V0 + dt.timedelta(days=7 * i)).isoformat() for i in range(1, 27)]
+    inp = dict(spot=100.0, strike=100.0, volatility=0.25, option_type="put",
+               barrier_type="down-and-out", lower_barrier=80.0, monitoring_dates=weekly,
+               flat_rate_nacc=0.05, num_space_nodes=n - 1, num_time_steps=40)
+    p = make(inp, Engine(), explicit_sign="corrected")
+    _, _, solves = p._grid_solves()
+    sv = solves[0]
+    assert sv.n_nodes == n and sv.ko_lo >= 0 and len(sv.mon_steps) > 0
+    plan = capi.vc_plan(n, B=B)
+    slots = 64 * plan["waves"] * plan["npt"]
+    if n in (257, 513, 1025, 2049, 4097, 8193) and B == 600:
+        assert slots == n - 1, plan  # the layout under test
+    ref = oracle_engine().run_vc([sv])[0]
+    gpu = Engine().run_vc([sv] * B)
+    scale = max(1.0, float(np.max(np.abs(ref))))
+    for g in (gpu[0], gpu[-1]):
+        assert float(np.max(np.abs(g - ref))) / scale <= 1e-10
+    assert all(np.array_equal(g, gpu[0]) for g in gpu)
