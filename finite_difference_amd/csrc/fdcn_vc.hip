@@ -98,6 +98,17 @@ __device__ __forceinline__ double from_above(double x, int d, int lane4) {
   return bperm(x, lane4 + 4 * d);
 }
 
+// 64-bit row-masked DPP move (two 32-bit moves): lanes without a source in
+// their row, and rows outside RM, receive 0
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp64(double x) {
+  const unsigned long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffull), CTRL, RM, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, RM, 0xF, true);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+constexpr int kRowShr = 0x110, kRowShl = 0x100, kRowBcast15 = 0x142, kRowBcast31 = 0x143;
+
 constexpr int kNC = 5;  // factored coefficients per slot: A, B, C, f, e
 
 struct VcArgs {
@@ -197,7 +208,17 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
   }
 
   double cA[NPT], cB[NPT], cC[NPT], cf[NPT], ce[NPT];
-  double FW[6], GW[6], Fpre = 0.0, Gsuf = 0.0, g0 = 0.0, gN = 0.0;
+  // The lane scans of the two recurrences run row-segmented: four DPP
+  // stages inside each 16-lane row, then the rows joined -- forward by
+  // row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3), backward by one
+  // ds_bpermute from the next row's first lane (rows 0, 2) and a readlane
+  // of lane 32 (rows 0, 1).  One LDS round trip per step instead of ten.
+  // Weights per stage: the products of the multipliers the stage spans.
+  double FR[4], GR[4], F16 = 0.0, F32 = 0.0, GA = 0.0, GB = 0.0;
+  const int rl = lane & 15;
+  int addrA = (lane & 16) == 0 ? (((lane | 15) + 1) << 2) : lane4;  // rows 0, 2 <- rows 1, 3
+  asm volatile("" : "+v"(addrA));
+  double Fpre = 0.0, Gsuf = 0.0, g0 = 0.0, gN = 0.0;
   // the zero-carry passes run as two half-chunk chains joined by the
   // multiplier product of the other half (upper half forward, lower half
   // backward): half the dependent FMA chain on a one-wave-per-SIMD kernel
@@ -231,11 +252,30 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
 #pragma unroll
       for (int k = 0; k < H; ++k) gl *= ce[k];
     }
+    {
+      double F = f, G = g, s;
+#define VC_ROW_STAGE(j)                                                   \
+      FR[j] = rl >= (1 << j) ? F : 0.0;                                   \
+      s = dpp64<kRowShr + (1 << j), 0xF>(F);                              \
+      F = rl >= (1 << j) ? F * s : F;                                     \
+      GR[j] = rl + (1 << j) <= 15 ? G : 0.0;                              \
+      s = dpp64<kRowShl + (1 << j), 0xF>(G);                              \
+      G = rl + (1 << j) <= 15 ? G * s : G;
+      VC_ROW_STAGE(0) VC_ROW_STAGE(1) VC_ROW_STAGE(2) VC_ROW_STAGE(3)
+#undef VC_ROW_STAGE
+      const bool odd = (lane & 16) != 0;
+      F16 = odd ? F : 0.0;
+      s = dpp64<kRowBcast15, 0xA>(F);
+      F = odd ? F * s : F;
+      F32 = lane >= 32 ? F : 0.0;
+      GA = odd ? 0.0 : G;
+      s = bperm(G, addrA);
+      G = odd ? G : G * s;
+      GB = lane < 32 ? G : 0.0;
+    }
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int d = 1 << j;
-      FW[j] = (lane >= d) ? f : 0.0;
-      GW[j] = (lane + d < 64) ? g : 0.0;
       const double fo = from_below(f, d, lane4), go = from_above(g, d, lane4);
       f = (lane >= d) ? f * fo : f;
       g = (lane + d < 64) ? g * go : g;
@@ -254,11 +294,17 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
   const int mend = mpos + __builtin_amdgcn_readfirstlane(I[FDCN_I_MON_COUNT]);
   while (mpos < mend && __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) < 1) ++mpos;
   int next_mon = mpos < mend ? __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) : 0x7fffffff;
+  // the next entry's step and rebate are fetched right after a projection
+  // (steps are strictly increasing, include/fdcn.h): the loads have a whole
+  // step to land instead of stalling the projection
+  double next_reb = mpos < mend ? uni(A.mon_rebate[mpos]) : 0.0;
 
   const double2* bnd = reinterpret_cast<const double2*>(A.bnd) + (size_t)scen * A.n_time;
   double2 bcur = make_double2(0.0, 0.0);
-  for (int m = 0; m < A.n_time; ++m) {
-    if (m == A.n_ranna && use_r && use_c) load_phase(1);
+  // one step; the march runs it in two loops (Rannacher phase, then CN) so
+  // the phase switch is not a branch in the step -- inside it the compiler
+  // if-converted the whole coefficient reload into every step
+  auto step = [&](int m) __attribute__((always_inline)) {
     if ((m & 63) == 0) {
       const int mm = m + lane;
       bcur = mm < A.n_time ? bnd[mm] : make_double2(0.0, 0.0);
@@ -296,8 +342,12 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
 #pragma unroll
       for (int k = 0; k < NPT; ++k) a = fma(cf[k], a, R[k]);
     }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) a = fma(FW[j], from_below(a, 1 << j, lane4), a);
+    a = fma(FR[0], dpp64<kRowShr + 1, 0xF>(a), a);
+    a = fma(FR[1], dpp64<kRowShr + 2, 0xF>(a), a);
+    a = fma(FR[2], dpp64<kRowShr + 4, 0xF>(a), a);
+    a = fma(FR[3], dpp64<kRowShr + 8, 0xF>(a), a);
+    a = fma(F16, dpp64<kRowBcast15, 0xA>(a), a);
+    a = fma(F32, dpp64<kRowBcast31, 0xC>(a), a);
     double cw = g0 * lo;  // carry into wave 0
     if constexpr (W > 1) {
       if (lane == 63) xch[2 * W + wave] = a;
@@ -332,8 +382,12 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
 #pragma unroll
       for (int k = NPT - 1; k >= 0; --k) b = fma(ce[k], b, R[k]);
     }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) b = fma(GW[j], from_above(b, 1 << j, lane4), b);
+    b = fma(GR[0], dpp64<kRowShl + 1, 0xF>(b), b);
+    b = fma(GR[1], dpp64<kRowShl + 2, 0xF>(b), b);
+    b = fma(GR[2], dpp64<kRowShl + 4, 0xF>(b), b);
+    b = fma(GR[3], dpp64<kRowShl + 8, 0xF>(b), b);
+    b = fma(GA, bperm(b, addrA), b);
+    b = fma(GB, read_lane(b, 32), b);
     double cwb = gN * hi;  // carry into the last wave
     if constexpr (W > 1) {
       if (lane == 0) xch[4 * W + wave] = b;
@@ -353,7 +407,7 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
 
     // ---- knock-out projection on monitoring steps --------------------------
     if (m + 1 == next_mon) {
-      double reb = uni(A.mon_rebate[mpos]);
+      double reb = next_reb;
       asm volatile("" : "+v"(reb));  // a VGPR copy: v_cndmask takes the mask as its SGPR operand
       const unsigned rlo = (unsigned)__double_as_longlong(reb);
       const unsigned rhi = (unsigned)(__double_as_longlong(reb) >> 32);
@@ -368,10 +422,17 @@ __global__ void __launch_bounds__(64 * W) fdcn_vc_march(VcArgs A) {
       }
       if (lo_out && ko0) v0 = reb;
       ++mpos;
-      while (mpos < mend && __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) <= m + 1) ++mpos;
       next_mon = mpos < mend ? __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) : 0x7fffffff;
+      next_reb = mpos < mend ? uni(A.mon_rebate[mpos]) : 0.0;
     }
     if constexpr (W > 1) __syncthreads();  // exchange area reused next step
+  };
+  const int m1 = (use_r && use_c) ? A.n_ranna : A.n_time;
+  int m = 0;
+  for (; m < m1; ++m) step(m);
+  if (m < A.n_time) {
+    load_phase(1);
+    for (; m < A.n_time; ++m) step(m);
   }
 
   double* vout = A.v_out + (size_t)scen * n;
@@ -393,9 +454,9 @@ VcVariant vmk() {
   return VcVariant{W, NPT, &fdcn_vc_march<W, NPT>};
 }
 // (W = 16 holds at most 128 VGPRs a wave and spills its NPT = 8 and 16
-// bodies; W = 8 keeps 256 and serves grids up to 8 193 nodes without)
+// bodies; W = 8 NPT = 16 (8 193 nodes) spills less, on half the waves)
 const VcVariant kVc[] = {vmk<1, 4>(),  vmk<1, 8>(),  vmk<1, 16>(), vmk<4, 4>(),
-                         vmk<4, 8>(),  vmk<4, 16>(), vmk<8, 8>(),  vmk<8, 16>(),
+                         vmk<4, 8>(),  vmk<4, 16>(), vmk<8, 16>(),
                          vmk<16, 4>(), vmk<16, 8>(), vmk<16, 16>()};
 constexpr int kNumVc = sizeof(kVc) / sizeof(kVc[0]);
 
