@@ -42,6 +42,14 @@ def _pmax(x: float, y: float) -> float:
     return y if y > x else x
 
 
+def _one_of(name_a: str, a, name_b: str, b):
+    """The value of whichever of two keyword spellings was given (the two
+    reference files spell the American pricer's arguments differently)."""
+    if a is not None and b is not None and a != b:
+        raise TypeError(f"got both {name_a}={a!r} and {name_b}={b!r}")
+    return a if a is not None else b
+
+
 class AmericanFDMPricer:
     """American vanilla option, Crank-Nicolson in log S with IT early exercise."""
 
@@ -481,8 +489,12 @@ class AmericanFDMPricer:
         applies the dividend jump, then segment i+1."""
         self._march_jobs(self._pending_jobs(requests), self._engine())
 
-    def _solve_grid(self, n_time: Optional[int] = None) -> List[float]:
-        """Value vector at valuation (fd_american_equity.py:778-843)."""
+    def _solve_grid(self, n_time: Optional[int] = None, *,
+                    N_time: Optional[int] = None) -> List[float]:
+        """Value vector at valuation (fd_american_equity.py:778-843).  Takes
+        the fd_american_equity.py spelling (n_time) and the
+        fd_american_option_pricer.py one (N_time, :659)."""
+        n_time = _one_of("n_time", n_time, "N_time", N_time)
         nt = self.num_time_steps if n_time is None else int(n_time)
         self.prefetch([(self.sigma, nt)])
         V, grid = self._cache[self._state_key(self.sigma, nt)]
@@ -626,11 +638,17 @@ class AmericanFDMPricer:
         _, b_coef, c_coef, _ = np.linalg.solve(design, yv)
         return float(c_coef), float(2.0 * b_coef)
 
-    def price_log(self, n_time: Optional[int] = None) -> float:
-        return self._interp_price(self._solve_grid(n_time=n_time))
+    def price_log(self, n_time: Optional[int] = None, *, N_time: Optional[int] = None) -> float:
+        """fd_american_equity.py:913 (n_time) and fd_american_option_pricer.py
+        :659 (N_time) spellings."""
+        return self._interp_price(self._solve_grid(n_time=_one_of("n_time", n_time,
+                                                                  "N_time", N_time)))
 
-    def price_log2(self, apply_ko: bool = True, use_richardson: bool = True) -> float:
-        """Richardson N vs 2*num_space_nodes (the reference's quirk, :950)."""
+    def price_log2(self, apply_ko: bool = True, use_richardson: bool = True, *,
+                   apply_KO: Optional[bool] = None) -> float:
+        """Richardson N vs 2*num_space_nodes (the reference's quirk, :950).
+        apply_ko / apply_KO (fd_american_option_pricer.py:663) are ignored,
+        as in both references."""
         if not use_richardson:
             return self.price_log(n_time=self.num_time_steps)
         if self._engine().on_device:
@@ -644,7 +662,9 @@ class AmericanFDMPricer:
         p_2n = self.price_log(n_time=2 * self.num_space_nodes)
         return (4.0 * p_2n - p_n) / 3.0
 
-    def _price_for_sigma(self, sigma: float, n_time: Optional[int] = None) -> float:
+    def _price_for_sigma(self, sigma: float, n_time: Optional[int] = None, *,
+                         N_time: Optional[int] = None) -> float:
+        n_time = _one_of("n_time", n_time, "N_time", N_time)
         original = self.sigma
         try:
             self.sigma = sigma

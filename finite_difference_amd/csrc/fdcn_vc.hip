@@ -297,8 +297,8 @@ __global__ void __launch_bounds__(64 * W, (W == 1 && NPT == 16) ? 2 : 1) fdcn_vc
   while (mpos < mend && __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) < 1) ++mpos;
   int next_mon = mpos < mend ? __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) : 0x7fffffff;
   // the next entry's step and rebate are fetched right after a projection
-  // (steps are strictly increasing, include/fdcn.h): the loads have a whole
-  // step to land instead of stalling the projection
+  // (entries at or before the step just projected are skipped there): the
+  // loads have a whole step to land instead of stalling the projection
   double next_reb = mpos < mend ? uni(A.mon_rebate[mpos]) : 0.0;
 
   const double2* bnd = reinterpret_cast<const double2*>(A.bnd) + (size_t)scen * A.n_time;
@@ -423,7 +423,10 @@ __global__ void __launch_bounds__(64 * W, (W == 1 && NPT == 16) ? 2 : 1) fdcn_vc
         V[k] = __longlong_as_double(((long long)hi32 << 32) | lo32);
       }
       if (lo_out && ko0) v0 = reb;
-      ++mpos;
+      // skip this entry and any repeat of it (the _dev entry point does not
+      // validate the runs; a repeated step would otherwise stall next_mon)
+      do ++mpos;
+      while (mpos < mend && __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) <= m + 1);
       next_mon = mpos < mend ? __builtin_amdgcn_readfirstlane(A.mon_step[mpos]) : 0x7fffffff;
       next_reb = mpos < mend ? uni(A.mon_rebate[mpos]) : 0.0;
     }

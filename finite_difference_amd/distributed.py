@@ -41,17 +41,32 @@ def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def _single_device_for_every_rank() -> bool:
+    """A rank other than local rank 0 that sees exactly one device may bind
+    it when the launcher evidently gave each rank its own GPU (a per-rank
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES, or one
+    rank per node), or when ranks are told to share it on purpose
+    (FDCN_SHARE_DEVICE=1: several ranks rehearsing the sharded path on one
+    GPU, tests/test_gpu_multirank.py)."""
+    if os.environ.get("FDCN_SHARE_DEVICE") == "1":
+        return True
+    if any(os.environ.get(v) for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                       "CUDA_VISIBLE_DEVICES")):
+        return True
+    return int(os.environ.get("LOCAL_WORLD_SIZE", "1")) <= 1
+
+
 def bind_device() -> Optional[int]:
     """One process per GPU: make this rank's GPU current for libfdcn (the
     host-array entry points run on the calling thread's HIP device) and for
     torch (RCCL collectives need it).  Local rank k binds the k-th visible
-    gfx950 device (its HIP ordinal may differ on a host with other GPUs);
-    when exactly one device is visible -- a launcher that hands each rank its
-    own GPU through HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES -- every rank
-    binds that one.  Returns the HIP ordinal, or None on a host with no
-    gfx950 device (CPU tests over gloo).  Raises if several devices are
-    visible but fewer than the local rank needs: every rank marching on GPU 0
-    is the failure this guards."""
+    gfx950 device (its HIP ordinal may differ on a host with other GPUs).
+    When exactly one device is visible every rank binds it only if the
+    launcher gave each rank its own (see _single_device_for_every_rank);
+    otherwise local ranks > 0 raise, as they do when several devices are
+    visible but fewer than the local rank needs: every rank silently marching
+    on GPU 0 is the failure this guards.  Returns the HIP ordinal, or None on
+    a host with no gfx950 device (CPU tests over gloo)."""
     from . import capi
     try:
         ords = capi.device_ordinals()
@@ -60,12 +75,15 @@ def bind_device() -> Optional[int]:
     if not ords:
         return None
     lr = local_rank()
-    if len(ords) == 1:
-        dev = ords[0]
-    elif lr < len(ords):
+    if lr < len(ords) and (len(ords) > 1 or lr == 0):
         dev = ords[lr]
+    elif len(ords) == 1 and _single_device_for_every_rank():
+        dev = ords[0]
     else:
-        raise capi.FdcnError(f"LOCAL_RANK={lr} but only {len(ords)} gfx950 device(s) are visible")
+        raise capi.FdcnError(
+            f"LOCAL_RANK={lr} (LOCAL_WORLD_SIZE={os.environ.get('LOCAL_WORLD_SIZE', '?')}) but "
+            f"only {len(ords)} gfx950 device(s) are visible; give each rank its own device "
+            f"(HIP_VISIBLE_DEVICES) or set FDCN_SHARE_DEVICE=1 to share one on purpose")
     capi.select_device(dev)
     try:
         import torch
@@ -123,8 +141,12 @@ def gather_columns(cols: dict) -> Optional[dict]:
     parts = [p for p in parts if p]  # a rank with no rows sends an empty dict
     if not parts:
         return {}
+    keys = list(parts[0])
+    for i, p in enumerate(parts[1:], 1):
+        if list(p) != keys:
+            raise ValueError(f"gather_columns: part {i} has columns {list(p)}, part 0 {keys}")
     out = {}
-    for k in parts[0]:
+    for k in keys:
         vals = [p[k] for p in parts]
         if all(isinstance(v, np.ndarray) for v in vals):
             out[k] = np.concatenate(vals)

@@ -314,6 +314,23 @@ def result_columns(cols: Dict[str, Sequence], res: Dict[str, np.ndarray]) -> Dic
     return out
 
 
+_LIST_KEYS = ("scenario_name", "S0", "K", "sigma", "rate", "barrier_type")
+
+
+def rows_as_result_columns(rows: List[Dict[str, Any]]) -> Dict[str, Any]:
+    """Per-row results (scenarios._result_row) as the columns result_columns
+    builds: same keys in the same order, lists for the six input keys and
+    float64 arrays for the rest -- so a shard priced by the per-row fallback
+    merges with shards priced here (distributed.gather_columns)."""
+    if not rows:
+        return {}
+    out: Dict[str, Any] = {}
+    for k in rows[0]:
+        vals = [r[k] for r in rows]
+        out[k] = vals if k in _LIST_KEYS else np.asarray(vals, np.float64)
+    return out
+
+
 ROW_KEYS = ("scenario_name", "S0", "K", "sigma", "rate", "barrier_type", "upper_barrier",
             "lower_barrier", "FA_price", "FA_delta", "FA_gamma", "FA_vega")
 

@@ -242,7 +242,7 @@ def run_all_scenarios(config_csv_path: str, output_csv_path: Optional[str],
         out = scenario_batch.result_columns(cols, priced)
     else:  # shapes the whole-file plan declines: the per-row facades, batched
         rows = run_rows_batched([dict(r) for _, r in part.iterrows()], base_params, engine)
-        out = {k: [r[k] for r in rows] for k in (rows[0] if rows else {})}
+        out = scenario_batch.rows_as_result_columns(rows)
     if sharded:
         out = distributed.gather_columns(out)
         if out is None:  # non-zero rank

@@ -315,7 +315,17 @@ class DiscreteBarrierFDMPricerAnalytic:
 
     def _continuous_leg(self, S_eff: float, sigma: float):
         """The continuous-window leg (:473-529): ("rr", contract),
-        ("douady", contract) or ("cn", None) for the every-step CN overlay."""
+        ("douady", contract) or ("cn", None) for the every-step CN overlay.
+        The reference wraps both engine calls in try/except and takes the CN
+        overlay when they raise (:486-519).  BarrierEngine raises on a
+        non-positive sigma or T and on the log of a non-positive level, so
+        such a contract goes to the overlay here -- e.g. greeks() with
+        abs_vol_bump >= volatility -- instead of failing the whole batch.
+        DoubleBarrier computes through NumPy and returns a number for a
+        negative sigma (no exception, no fallback): kept, fixture
+        dko_daily_douady_vol_bump_past_zero."""
+        def positive(*xs):
+            return all(math.isfinite(x) and x > 0.0 for x in xs)
         if self.barrier_type in ("double-out", "double-in"):
             if (not self.double_barrier_analytic or self.bgk_lower_barrier is None
                     or self.bgk_upper_barrier is None):
@@ -329,7 +339,7 @@ class DiscreteBarrierFDMPricerAnalytic:
             return ("cn", None)
         down = "down" in self.barrier_type
         H = self.bgk_lower_barrier if down else self.bgk_upper_barrier
-        if H is None:
+        if H is None or not positive(S_eff, self.strike, H, sigma, self.tenor_years):
             return ("cn", None)
         return ("rr", dict(s=S_eff, b=self.flat_carry_b, r=self.flat_rate_r, t=self.tenor_years,
                            x=self.strike, sigma=sigma, h=H,

@@ -578,6 +578,17 @@ def gen_spot_analytic():
              barrier_type="double-in", strike=100.0, lower_barrier=82.0, upper_barrier=120.0,
              spot=100.0, volatility=0.2, monitoring_dates=daily, rate=0.05, time_steps=6,
              space_nodes=150, n_desired_for_decision=20),
+        # greeks() with abs_vol_bump > volatility: the sigma-down repricing's
+        # BarrierEngine raises and the reference falls back to the CN overlay
+        # (:486-519); the Douady case likewise if DoubleBarrier raises
+        dict(name="call_uo_daily_rr_vol_bump_past_zero", option_type="call",
+             barrier_type="up-and-out", strike=100.0, lower_barrier=None, upper_barrier=130.0,
+             spot=100.0, volatility=0.25, monitoring_dates=daily, rate=0.05, time_steps=10,
+             space_nodes=150, n_desired_for_decision=20, greeks_kw=dict(abs_vol_bump=0.3)),
+        dict(name="dko_daily_douady_vol_bump_past_zero", douady=True, option_type="call",
+             barrier_type="double-out", strike=100.0, lower_barrier=80.0, upper_barrier=125.0,
+             spot=100.0, volatility=0.2, monitoring_dates=daily, rate=0.05, time_steps=6,
+             space_nodes=150, n_desired_for_decision=20, greeks_kw=dict(abs_vol_bump=0.25)),
         dict(name="vanilla_put", option_type="put", barrier_type="none", strike=100.0,
              lower_barrier=None, upper_barrier=None, spot=100.0, volatility=0.25,
              monitoring_dates=[], rate=0.05, time_steps=6, space_nodes=150,
@@ -586,7 +597,8 @@ def gen_spot_analytic():
     cases = []
     for sp in specs:
         kw = dict(base)
-        kw.update({k: v for k, v in sp.items() if k not in ("name", "rate", "divs", "douady")})
+        kw.update({k: v for k, v in sp.items()
+                   if k not in ("name", "rate", "divs", "douady", "greeks_kw")})
         c = curve(sp["rate"])
         kw["discount_curve"] = c
         kw["forward_curve"] = c
@@ -620,7 +632,7 @@ def gen_spot_analytic():
             p.spot_grid = grid0
             p.grid_step_dS = p.spot_grid[1] - p.spot_grid[0]
             rec["price"] = p.price()
-            rec["greeks"] = p.greeks()
+            rec["greeks"] = p.greeks(**sp.get("greeks_kw", {}))
         finally:
             m.DoubleBarrier = shipped_db
         cases.append(rec)

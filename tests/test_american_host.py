@@ -94,3 +94,20 @@ def test_native_dividend_jump_is_bitwise_numpy():
             a = p._apply_dividend_jump(v, D)
             b = p._apply_dividend_jump_numpy(v, D)
             assert [x.hex() for x in a] == [float(x).hex() for x in b], (case["name"], D)
+
+
+def test_both_reference_spellings():
+    """fd_american_option_pricer.py:659-680 spells the arguments N_time /
+    apply_KO, fd_american_equity.py:913-925 n_time / apply_ko: both work on
+    AmericanFDMPricer and give == results (VERDICT r3 missing #1)."""
+    case = CASES[0]
+    p = make(case, oracle_engine())
+    n = case["inputs"]["M"]
+    assert p.price_log(N_time=n) == p.price_log(n_time=n) == p.price_log(n)
+    assert p.price_log(N_time=2 * n) == p.price_log(n_time=2 * n)
+    assert p._solve_grid(N_time=n) == p._solve_grid(n_time=n) == p._solve_grid()
+    assert p.price_log2(apply_KO=True) == p.price_log2(apply_ko=True) == case["price_log2"]
+    assert p.price_log2(apply_KO=False, use_richardson=False) == p.price_log()
+    assert p._price_for_sigma(p.sigma + 0.01, N_time=n) == p._price_for_sigma(p.sigma + 0.01, n)
+    with pytest.raises(TypeError):
+        p.price_log(n, N_time=n + 1)

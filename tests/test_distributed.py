@@ -25,12 +25,14 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, decline_rank=-1):
     import sys
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
     from backends import oracle_engine
-    from finite_difference_amd import scenarios
+    from finite_difference_amd import scenario_batch, scenarios
+    if rank == decline_rank:  # this shard takes the per-row fallback
+        scenario_batch.price_columns = lambda *a, **k: None
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     try:
@@ -69,16 +71,68 @@ def test_two_rank_gloo_matches_single_process(tmp_path):
         assert (got[col].to_numpy() == ref[col].to_numpy()).all(), col
 
 
+def test_two_rank_gloo_one_shard_on_the_fallback(tmp_path):
+    """Rank 1's whole-file plan is declined, so its shard goes through the
+    per-row façades (run_rows_batched) while rank 0's takes price_columns:
+    the merged columns have one schema and equal the single-process run."""
+    from backends import oracle_engine
+    from finite_difference_amd import scenarios
+    out = str(tmp_path / "dist.csv")
+    mp.start_processes(_worker, args=(2, _free_port(), out, 1), nprocs=2, join=True,
+                       start_method="spawn")
+    single = scenarios.run_all_scenarios(CFG, None, scenarios.runner_base_params("put", 60),
+                                         engine=oracle_engine(), verbose=False)
+    got = pd.read_csv(out, float_precision="round_trip")
+    ref = single.reset_index(drop=True)
+    assert list(got.columns) == list(ref.columns)
+    assert list(got["scenario_name"]) == list(ref["scenario_name"])
+    for col in ("model_price", "model_delta", "model_gamma", "model_vega"):
+        assert (got[col].to_numpy() == ref[col].to_numpy()).all(), col
+
+
+def test_gather_columns_rejects_mismatched_parts(monkeypatch):
+    class FakeDist:
+        def get_rank(self):
+            return 0
+
+        def get_world_size(self):
+            return 2
+
+        def gather_object(self, obj, out, dst=0):
+            out[0] = obj
+            out[1] = {"b": [1], "a": [2]}
+    monkeypatch.setattr(fdist, "_dist", lambda: FakeDist())
+    with pytest.raises(ValueError):
+        fdist.gather_columns({"a": [1], "b": [2]})
+
+
 def test_bind_device_maps_local_rank_through_gfx950_ordinals(monkeypatch):
-    """ADVICE r2: local rank k binds the k-th visible gfx950 device; a rank
-    that sees exactly one device (HIP_VISIBLE_DEVICES per rank) binds it
-    whatever its LOCAL_RANK; too few devices for the rank is an error."""
+    """ADVICE r2/r3: local rank k binds the k-th visible gfx950 device; a rank
+    that sees exactly one device binds it whatever its LOCAL_RANK only when
+    the launcher gave each rank its own (per-rank HIP_VISIBLE_DEVICES, one
+    rank per node) or sharing is asked for (FDCN_SHARE_DEVICE=1); too few
+    devices for the rank is an error."""
     from finite_difference_amd import capi
     chosen = []
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+              "FDCN_SHARE_DEVICE", "LOCAL_WORLD_SIZE"):
+        monkeypatch.delenv(v, raising=False)
     monkeypatch.setattr(capi, "select_device", lambda d: chosen.append(d))
     monkeypatch.setattr(capi, "device_ordinals", lambda: [0])
-    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("LOCAL_RANK", "0")
     assert fdist.bind_device() == 0 and chosen[-1] == 0
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    with pytest.raises(capi.FdcnError):  # torchrun --nproc-per-node 2 on one visible GPU
+        fdist.bind_device()
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")  # the launcher's per-rank device
+    assert fdist.bind_device() == 0 and chosen[-1] == 0
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.setenv("FDCN_SHARE_DEVICE", "1")
+    assert fdist.bind_device() == 0
+    monkeypatch.delenv("FDCN_SHARE_DEVICE")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert fdist.bind_device() == 0
     monkeypatch.setattr(capi, "device_ordinals", lambda: [1, 3, 4])
     assert fdist.bind_device() == 3 and chosen[-1] == 3
     monkeypatch.setenv("LOCAL_RANK", "3")

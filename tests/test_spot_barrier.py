@@ -136,20 +136,31 @@ def test_spot_price_on_gpu_matches_black_scholes():
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [257, 513, 1024, 1025, 1026, 2049, 4097, 4098, 8193])
 @pytest.mark.parametrize("B", [1, 600])
-def test_spot_kernel_grid_one_node_longer_than_the_slots(n, B):
+@pytest.mark.parametrize("bt", ["down-and-out", "up-and-out", "none"])
+def test_spot_kernel_grid_one_node_longer_than_the_slots(n, B, bt):
     """N + 1 nodes on N = 64 W NPT slots (1 025 = the reference's 1 024-step
     grid): node 0 stays outside the slots as a scalar (fdcn_vc pad_lo = -1).
     A down-and-out knocks node 0 out on every weekly date, so the scalar's
-    projection is covered; n = slots and slots + 2 keep the padded layout."""
+    projection is covered; an up-and-out and a vanilla keep node 0 at its
+    Dirichlet value on every step (ADVICE r3), on every layout W = 1 / 4 / 8;
+    n = slots and slots + 2 keep the padded layout."""
     from finite_difference_amd import capi
+    if bt != "down-and-out" and n not in (1025, 4097, 8193):
+        pytest.skip("the node-0-outside layouts only")
     weekly = [(V0 + dt.timedelta(days=7 * i)).isoformat() for i in range(1, 27)]
     inp = dict(spot=100.0, strike=100.0, volatility=0.25, option_type="put",
-               barrier_type="down-and-out", lower_barrier=80.0, monitoring_dates=weekly,
+               barrier_type=bt, lower_barrier=80.0 if bt == "down-and-out" else None,
+               upper_barrier=125.0 if bt == "up-and-out" else None,
+               monitoring_dates=weekly if bt != "none" else [],
                flat_rate_nacc=0.05, num_space_nodes=n - 1, num_time_steps=40)
     p = make(inp, Engine(), explicit_sign="corrected")
     _, _, solves = p._grid_solves()
     sv = solves[0]
-    assert sv.n_nodes == n and sv.ko_lo >= 0 and len(sv.mon_steps) > 0
+    assert sv.n_nodes == n
+    if bt == "down-and-out":
+        assert sv.ko_lo >= 0 and len(sv.mon_steps) > 0
+    elif bt == "up-and-out":
+        assert sv.ko_lo < 0 and sv.ko_hi < n and len(sv.mon_steps) > 0
     plan = capi.vc_plan(n, B=B)
     slots = 64 * plan["waves"] * plan["npt"]
     if n in (257, 513, 1025, 2049, 4097, 8193) and B == 600:
@@ -159,4 +170,51 @@ def test_spot_kernel_grid_one_node_longer_than_the_slots(n, B):
     scale = max(1.0, float(np.max(np.abs(ref))))
     for g in (gpu[0], gpu[-1]):
         assert float(np.max(np.abs(g - ref))) / scale <= 1e-10
+        assert g[0] == ref[0]  # node 0 (the scalar) exactly its Dirichlet / rebate value
     assert all(np.array_equal(g, gpu[0]) for g in gpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1025, 600])
+def test_spot_dev_entry_skips_repeated_monitor_steps(n):
+    """fdcn_vc_batch_dev does not validate the monitor
+    runs; a repeated or out-of-order step is skipped (the oracle's `while`)
+    instead of stalling every later projection of that scenario."""
+    import dataclasses
+
+    import torch
+    from finite_difference_amd import capi
+    from finite_difference_amd.engine import pack_vc
+    from oracle import oracle
+    inp = dict(spot=100.0, strike=100.0, volatility=0.25, option_type="call",
+               barrier_type="double-out", lower_barrier=85.0, upper_barrier=120.0,
+               monitoring_dates=[], flat_rate_nacc=0.05, num_space_nodes=n - 1,
+               num_time_steps=60)
+    p = make(inp, Engine(), explicit_sign="corrected")
+    sv = p._grid_solves()[2][0]
+    sv.ko_lo, sv.ko_hi = p._ko_nodes(p._grid_solves()[0], 85.0, 120.0)
+    runs = [[3, 3, 8, 5, 12, 12, 12, 30, 60], [7, 2, 7, 40, 41, 41, 60]]
+    solves = []
+    for r in runs:
+        solves.append(dataclasses.replace(sv, mon_steps=r,
+                                          mon_rebates=[0.25 * (k + 1) for k in range(len(r))]))
+    g = pack_vc(solves, [0, 1])
+    dev = torch.device("cuda", 0)
+    T = {k: torch.from_numpy(np.ascontiguousarray(getattr(g, k))).to(dev)
+         for k in ("diag", "bnd", "v_init", "iparams", "mon_step", "mon_rebate")}
+    out = torch.empty_like(T["v_init"])
+    wsb = capi.vc_plan(g.n_nodes, B=g.B)["ws_bytes_per_scen"] * g.B
+    ws = torch.empty(wsb // 8 + 1, dtype=torch.float64, device=dev)
+    capi.vc_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, T["diag"].data_ptr(),
+                      T["bnd"].data_ptr(), T["v_init"].data_ptr(), T["iparams"].data_ptr(),
+                      len(g.mon_step), T["mon_step"].data_ptr(), T["mon_rebate"].data_ptr(),
+                      out.data_ptr(), ws.data_ptr(), wsb, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    ref = oracle.vc_batch(g.n_nodes, g.n_time, g.n_ranna, g.diag, g.bnd, g.v_init, g.iparams,
+                          g.mon_step, g.mon_rebate)
+    for b in range(2):
+        scale = max(1.0, float(np.max(np.abs(ref[b]))))
+        assert float(np.max(np.abs(got[b] - ref[b]))) / scale <= 1e-10, b
+    # the last projection of each run took effect: knocked-out nodes hold its rebate
+    assert got[0][0] == 0.25 * 9 and got[1][-1] == 0.25 * 7

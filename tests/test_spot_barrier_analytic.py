@@ -44,6 +44,7 @@ def make(case, engine, **extra):
     rate = inp.pop("rate")
     divs = inp.pop("divs", [])
     douady = inp.pop("douady", False)
+    inp.pop("greeks_kw", None)
     c = market.create_rate_df(rate)
     c["Date"] = pd.to_datetime(c["Date"], format="%Y/%m/%d").dt.strftime("%Y-%m-%d")
     kw = dict(trade_id="T1", direction="long", quantity=1, contract_multiplier=1.0,
@@ -104,7 +105,7 @@ def test_cn_stepper_vectors_bitwise(case):
 @pytest.mark.parametrize("case", CASES, ids=lambda c: c["name"])
 def test_price_and_greeks_vs_reference(case):
     p = make(case, oracle_engine())
-    price, greeks = p.price(), p.greeks()
+    price, greeks = p.price(), p.greeks(**case["inputs"].get("greeks_kw", {}))
     if not _analytic_leg(p):
         assert price == case["price"]
         assert greeks == case["greeks"]
@@ -159,7 +160,8 @@ def test_gpu_facade_vs_oracle_facade(case):
     growth = max(1.0, max(abs(x) for x in case["V_vanilla"]))
     pg, pr = gpu.price(), ref.price()
     assert abs(pg - pr) <= 1e-9 * growth, (pg, pr)
-    gg, gr = gpu.greeks(), ref.greeks()
+    gkw = case["inputs"].get("greeks_kw", {})
+    gg, gr = gpu.greeks(**gkw), ref.greeks(**gkw)
     assert abs(gg["delta"] - gr["delta"]) <= 1e-7 * growth
     assert abs(gg["vega"] - gr["vega"]) <= 1e-5 * growth
     assert abs(gg["gamma"] - gr["gamma"]) <= 1e-3 * growth
