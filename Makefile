@@ -11,6 +11,10 @@
 #                   (-fno-sanitize-recover: the first report aborts), linked
 #                   with the regular device objects into build/asan/libfdcn.so;
 #                   the bitwise plan tests then run against it
+#                   then tools/sanitize/session_book_driver.cpp: the device
+#                   sessions' host-only bookkeeping (csrc/fdcn_session_book.h:
+#                   pinned staging arena, slot and event tables) under the same
+#                   two sanitizers, malloc standing in for hipHostMalloc
 #   make tsan       the same two units under ThreadSanitizer with
 #                   tools/sanitize/plan_driver.cpp: the plan builders' worker
 #                   threads, two callers at once
@@ -24,7 +28,7 @@ ASAN := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
 TSAN := -Xarch_host -fsanitize=thread
 CSRC := finite_difference_amd/csrc
 HOST_SRCS := $(CSRC)/fdcn_host.hip $(CSRC)/fdcn_plan.hip
-HDRS := include/fdcn.h include/fdcn_diag.h $(CSRC)/fdcn_shared.h
+HDRS := include/fdcn.h include/fdcn_diag.h $(CSRC)/fdcn_shared.h $(CSRC)/fdcn_session_book.h
 DEV_OBJS := build/obj/fdcn_kernels.o build/obj/fdcn_analytic.o build/obj/fdcn_session.o \
             build/obj/fdcn_vc.o
 SAN_TESTS := tests/test_tau_sequence.py tests/test_capi_symbols.py tests/test_scenario_batch.py \
@@ -44,7 +48,14 @@ build/asan/%.o: $(CSRC)/%.hip $(HDRS)
 build/asan/libfdcn.so: build/asan/fdcn_host.o build/asan/fdcn_plan.o $(DEV_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -shared-libsan $(ASAN) -o $@ $^
 
-asan: build/asan/libfdcn.so
+build/asan/session_book_driver: tools/sanitize/session_book_driver.cpp $(CSRC)/fdcn_session_book.h
+	@mkdir -p build/asan
+	$(CXX) -std=c++17 -g -O1 -Wall -fsanitize=address,undefined -fno-sanitize-recover=all \
+	    -fno-omit-frame-pointer -o $@ $<
+
+asan: build/asan/libfdcn.so build/asan/session_book_driver
+	ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
+	    ./build/asan/session_book_driver
 	LD_PRELOAD=$(ASAN_RT) ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0:abort_on_error=1 \
 	UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
 	$(PY) -m pytest $(SAN_TESTS) -q -x -p no:cacheprovider --fdcn-lib build/asan/libfdcn.so

@@ -98,6 +98,10 @@ def parse(argv=None):
                     help="strong scaling (BASELINE config 4): ONE batch of this many scenarios, "
                          "built identically on every rank; rank r marches its contiguous "
                          "shard (distributed.shard_range)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group of the N>1 ranks: nccl (RCCL over xGMI, one GPU per "
+                         "rank) or gloo (host collectives: ranks rehearsing the sharded path "
+                         "on one GPU with FDCN_SHARE_DEVICE=1, tests/test_gpu_multirank.py)")
     ap.add_argument("--lib", default="", help="A/B timing: load this build of libfdcn.so")
     ap.add_argument("--force-variant", default="",
                     help="A/B timing: W,NPT[,FLAVOUR] pinned through fdcn_force_variant "
@@ -458,10 +462,14 @@ def run_rank(args):
         raise capi.FdcnError("no gfx950 device visible; the benchmark needs an MI355X")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", bound))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", bound))
+        else:
+            dist.init_process_group("gloo")
     if args.force_variant:
         capi.force_variant(*[int(x) for x in args.force_variant.split(",")])
     dev = torch.device("cuda", bound)
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")  # collective tensors
     builder, ns0, nt0, is_it, label = WORKLOADS[args.workload]
     n_space, n_time = args.n_space or ns0, args.n_time or nt0
     t_build = time.perf_counter()
@@ -526,9 +534,9 @@ def run_rank(args):
     # at most under --total), summed over the ranks
     node_steps_launch = g.B * node_units(g) * g.n_time  # configured nodes x steps x solves
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        tot = torch.tensor([float(node_steps_launch)], dtype=torch.float64, device=dev)
+        tot = torch.tensor([float(node_steps_launch)], dtype=torch.float64, device=cdev)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         elapsed = float(t.item())
         job_node_steps = float(tot.item())
@@ -553,11 +561,13 @@ def run_rank(args):
     elif world > 1 and not args.no_cpu_baseline:
         # every rank checks a sample of its own timed output against the C
         # oracle on its host cores; the record is the worst over the ranks
-        parity = reduce_parity(sample_parity(g, res, PARITY_SAMPLE), world, dev)
+        parity = reduce_parity(sample_parity(g, res, PARITY_SAMPLE), world, cdev)
 
     if rank == 0:
         config = {"workload": workload, "scenarios_per_gpu": g.B, "grid": [n_space, n_time],
                   "parallelism": f"scenario-sharded x{world}"}
+        if world > 1:
+            config["process_group"] = args.backend
         if args.total:
             config.update(total_scenarios=args.total, shard="contiguous (shard_range)")
         if is_it:
@@ -686,6 +696,11 @@ def bench_scenario_file(args):
                               for b, x in zip(bt, rng.uniform(0.6, 0.98, R) * S0)],
             "FA_price": [1.0] * R, "FA_delta": [0.5] * R, "FA_gamma": [0.01] * R,
             "FA_vega": [0.2] * R}
+    # the columns as run_all_scenarios hands them over (DataFrame columns as
+    # NumPy arrays; a missing barrier level is NaN, as pandas reads the CSV)
+    cols = {k: np.asarray([np.nan if v is None else v for v in c],
+                          dtype=object if k in ("scenario_name", "barrier_type") else np.float64)
+            for k, c in cols.items()}
     base = scenarios.runner_base_params("put", N)
     base.update(num_time_steps=M, grid_mode="explicit")
     eng = Engine()

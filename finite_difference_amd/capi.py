@@ -44,7 +44,8 @@ EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batc
             "fdcn_vc_batch", "fdcn_vc_batch_dev", "fdcn_vc_plan", "fdcn_barrier_plan",
             "fdcn_vmath", "fdcn_american_plan", "fdcn_device_ordinals")
 # include/fdcn_diag.h: test / tuning entry points, not the product boundary
-DIAG_EXPORTED = ("fdcn_force_variant", "fdcn_forced_variant", "fdcn_variant_name")
+DIAG_EXPORTED = ("fdcn_force_variant", "fdcn_forced_variant", "fdcn_variant_name",
+                 "fdcn_vc_force_variant", "fdcn_vc_variant_name", "fdcn_vc_forms")
 FLAVOUR_THROUGHPUT, FLAVOUR_LATENCY, FLAVOUR_PAIRED = 0, 1, 2
 VC_NDIAG = 6
 RR_NPARAM, RR_NFLAG = 8, 5
@@ -215,6 +216,12 @@ def lib() -> ctypes.CDLL:
             L.fdcn_forced_variant.argtypes = [_PI, _PI, _PI]
             L.fdcn_variant_name.restype = _I
             L.fdcn_variant_name.argtypes = [_I, _I, _I, _I, ctypes.c_char_p, _I]
+            L.fdcn_vc_force_variant.restype = _I
+            L.fdcn_vc_force_variant.argtypes = [_I, _I, _I]
+            L.fdcn_vc_variant_name.restype = _I
+            L.fdcn_vc_variant_name.argtypes = [_I, _I, ctypes.c_char_p, _I]
+            L.fdcn_vc_forms.restype = _I
+            L.fdcn_vc_forms.argtypes = [_I, _I, _I, _I, _PD, _PI]
             if L.fdcn_abi_version() != ABI_VERSION:
                 raise FdcnError("libfdcn.so ABI version mismatch; rebuild")
             _lib = L
@@ -392,6 +399,30 @@ def vc_plan(n_nodes: int, *, B: int) -> dict:
     ws = ctypes.c_int64()
     _check(lib().fdcn_vc_plan(B, n_nodes, ctypes.byref(w), ctypes.byref(npt), ctypes.byref(ws)))
     return dict(waves=w.value, npt=npt.value, ws_bytes_per_scen=ws.value)
+
+
+def vc_force_variant(waves: int = 0, npt: int = 0, stencil_only: bool = False) -> None:
+    """Diagnostics (include/fdcn_diag.h): pin later fdcn_vc launches to the
+    compiled variant (waves, npt) where it fits, and/or make every scenario
+    take the stencil form; (0, 0, False) clears.  Tests and A/B tools only."""
+    _check(lib().fdcn_vc_force_variant(int(waves), int(npt), 1 if stencil_only else 0))
+
+
+def vc_variant_name(n_nodes: int, *, B: int) -> str:
+    buf = ctypes.create_string_buffer(64)
+    _check(lib().fdcn_vc_variant_name(int(B), int(n_nodes), buf, 64))
+    return buf.value.decode()
+
+
+def vc_forms(n_nodes: int, n_time: int, n_ranna: int, diag: np.ndarray) -> np.ndarray:
+    """Form each scenario of a fdcn_vc launch takes (1 pointwise, 0 stencil):
+    the factor kernel's classification of diag [B, 2, 6, n_nodes], on the host."""
+    D = _f64(diag)
+    B = D.shape[0]
+    out = np.zeros(B, np.int32)
+    _check(lib().fdcn_vc_forms(B, int(n_nodes), int(n_time), int(n_ranna),
+                               D.ctypes.data_as(_PD), out.ctypes.data_as(_PI)))
+    return out
 
 
 VM_EXP, VM_LOG, VM_SQRT, VM_SQUARE = 0, 1, 2, 3

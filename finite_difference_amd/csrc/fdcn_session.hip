@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "../../include/fdcn.h"
+#include "fdcn_session_book.h"
 
 namespace fdcn_internal {
 int set_error(int code, const char* msg);
@@ -90,17 +91,8 @@ int sfail(int code, const char* fmt, ...) {
   } while (0)
 
 constexpr int kMaxStreams = 4;
-size_t al256(size_t n) { return (n + 255) / 256 * 256; }
-
-// Layout helper: offsets of consecutive 256-byte-aligned sub-buffers.
-struct Layout {
-  size_t size = 0;
-  size_t add(size_t bytes) {
-    const size_t o = size;
-    size += al256(bytes > 0 ? bytes : 1);
-    return o;
-  }
-};
+using fdcn_book::al256;
+using fdcn_book::Layout;
 
 // ---------------------------------------------------------------------------
 // kernels
@@ -333,44 +325,18 @@ int readouts_per_kind(int kind) {
   }
 }
 
-// Pinned staging: within a session every async copy reads/writes a region no
-// later call of that session reuses; the regions are recycled only after
-// fdcn_session_destroy has synchronised the session's streams.
-struct PinnedArena {
-  struct Chunk {
-    char* p;
-    size_t cap;
-  };
-  std::vector<Chunk> chunks;
-  size_t cur = 0, used = 0;
-  char* get(size_t bytes) {
-    bytes = al256(bytes > 0 ? bytes : 1);
-    while (cur < chunks.size() && used + bytes > chunks[cur].cap) {
-      ++cur;
-      used = 0;
-    }
-    if (cur == chunks.size()) {
-      const size_t sz = std::max(bytes, (size_t)8 << 20);
-      char* p = nullptr;
-      if (hipHostMalloc((void**)&p, sz, hipHostMallocDefault) != hipSuccess) return nullptr;
-      chunks.push_back({p, sz});
-      used = 0;
-    }
-    char* r = chunks[cur].p + used;
-    used += bytes;
-    return r;
+// Pinned staging (fdcn_session_book.h): within a session every async copy
+// reads/writes a region no later call of that session reuses; the regions
+// are recycled only after fdcn_session_destroy has synchronised the
+// session's streams.
+struct HipPinned {
+  static void* alloc(size_t n) {
+    void* p = nullptr;
+    return hipHostMalloc(&p, n, hipHostMallocDefault) == hipSuccess ? p : nullptr;
   }
-  void reset() { cur = used = 0; }
-  // Unpin the chunks beyond the first `keep` bytes (after reset: nothing in
-  // use).  A whole-file plan stages hundreds of MB; an idle context keeps
-  // only what a typical trade needs, not the largest file ever staged.
-  void trim(size_t keep) {
-    size_t held = 0, k = 0;
-    while (k < chunks.size() && held + chunks[k].cap <= keep) held += chunks[k++].cap;
-    for (size_t i = k; i < chunks.size(); ++i) (void)hipHostFree(chunks[i].p);
-    chunks.resize(k);
-  }
+  static void release(void* p) { (void)hipHostFree(p); }
 };
+using PinnedArena = fdcn_book::PinnedArenaT<HipPinned>;
 // pinned staging an idle per-thread context keeps between sessions: enough
 // for a whole-file plan (a 10 000-row barrier file stages 131 MB, a 2 000-row
 // American file ~400 MB), so repeated files reuse it (pinning it again costs
@@ -399,9 +365,7 @@ struct fdcn_session {
   std::vector<hipStream_t> streams;  // the ctx streams this session has used
   int rr = 0;
   std::vector<hipEvent_t> events;
-  std::vector<double*> slot_ptr;
-  std::vector<int32_t> slot_n;
-  std::vector<int32_t> slot_ev;
+  fdcn_book::SlotTable slots;
   struct Block {
     void* p;
     hipStream_t s;
@@ -430,23 +394,14 @@ int pick_stream(fdcn_session* s, hipStream_t* out) {
 }
 
 int check_slots(fdcn_session* s, int32_t n, const int32_t* slots, int32_t n_nodes) {
-  for (int32_t i = 0; i < n; ++i) {
-    const int32_t k = slots[i];
-    if (k < 0 || k >= (int32_t)s->slot_ptr.size())
-      return sfail(FDCN_EINVAL, "slot %d does not exist (session has %zu)", k, s->slot_ptr.size());
-    if (n_nodes >= 0 && s->slot_n[k] != n_nodes)
-      return sfail(FDCN_EINVAL, "slot %d holds %d nodes, expected %d", k, s->slot_n[k], n_nodes);
-  }
+  char err[160];
+  if (s->slots.check(n, slots, n_nodes, err, sizeof(err))) return sfail(FDCN_EINVAL, "%s", err);
   return FDCN_OK;
 }
 
 // make `st` wait for the launches that produced the given slots
 int wait_producers(fdcn_session* s, hipStream_t st, int32_t n, const int32_t* slots) {
-  std::vector<int32_t> evs;
-  for (int32_t i = 0; i < n; ++i) evs.push_back(s->slot_ev[slots[i]]);
-  std::sort(evs.begin(), evs.end());
-  evs.erase(std::unique(evs.begin(), evs.end()), evs.end());
-  for (int32_t e : evs) S_TRY(hipStreamWaitEvent(st, s->events[e], 0));
+  for (int32_t e : s->slots.producers(n, slots)) S_TRY(hipStreamWaitEvent(st, s->events[e], 0));
   return FDCN_OK;
 }
 
@@ -477,12 +432,7 @@ int record(fdcn_session* s, hipStream_t st, int32_t* ev) {
 
 int new_slots(fdcn_session* s, double* base, int32_t B, int32_t n_nodes, int32_t ev,
               int32_t* out_slots) {
-  for (int32_t b = 0; b < B; ++b) {
-    out_slots[b] = (int32_t)s->slot_ptr.size();
-    s->slot_ptr.push_back(base + (size_t)b * n_nodes);
-    s->slot_n.push_back(n_nodes);
-    s->slot_ev.push_back(ev);
-  }
+  s->slots.add(base, B, n_nodes, ev, out_slots);
   return FDCN_OK;
 }
 
@@ -550,7 +500,7 @@ int fdcn_session_destroy(fdcn_session* s) {
   return rc;
 }
 
-int fdcn_session_slots(const fdcn_session* s) { return s ? (int)s->slot_ptr.size() : -1; }
+int fdcn_session_slots(const fdcn_session* s) { return s ? (int)s->slots.size() : -1; }
 
 int fdcn_session_march(fdcn_session* s, int32_t it, int32_t B, int32_t n_nodes, int32_t n_time,
                        int32_t n_ranna, const double* params, const int32_t* iparams,
@@ -603,7 +553,7 @@ int fdcn_session_march(fdcn_session* s, int32_t it, int32_t B, int32_t n_nodes, 
   if (it) stage_copy(h + oF, payoff, sizeof(double) * nv);
   if (v_init_slots) {
     uint64_t* a = (uint64_t*)(h + oA);
-    for (int32_t b = 0; b < B; ++b) a[b] = (uint64_t)s->slot_ptr[v_init_slots[b]];
+    for (int32_t b = 0; b < B; ++b) a[b] = (uint64_t)s->slots.ptr[v_init_slots[b]];
   } else if (!v_is_payoff) {
     stage_copy(h + oV, v_init, sizeof(double) * nv);
   }
@@ -658,7 +608,7 @@ int fdcn_session_dividend_jump(fdcn_session* s, int32_t B, int32_t n_nodes,
   char* h = s->pinned().get(staged);
   if (!h) return sfail(FDCN_ENOMEM, "hipHostMalloc(%zu) failed", staged);
   uint64_t* a = (uint64_t*)(h + oA);
-  for (int32_t b = 0; b < B; ++b) a[b] = (uint64_t)s->slot_ptr[in_slots[b]];
+  for (int32_t b = 0; b < B; ++b) a[b] = (uint64_t)s->slots.ptr[in_slots[b]];
   stage_copy(h + oS, s_nodes, sizeof(double) * nv);
   memcpy(h + oC, cash_div, sizeof(double) * B);
   memcpy(h + oK, strike_call, sizeof(double) * B);
@@ -697,7 +647,7 @@ int fdcn_session_greeks(fdcn_session* s, int32_t T, const int32_t* kind, const i
     slots[r] = ri[0];
     int rc = check_slots(s, 1, &ri[0], -1);
     if (rc) return rc;
-    const int n = s->slot_n[ri[0]];
+    const int n = s->slots.n[ri[0]];
     const bool ok_i = (ri[1] == 1) || (ri[1] == 2 && ri[2] >= 0 && ri[2] < n) ||
                       (ri[1] == 0 && ri[2] >= 0 && ri[2] + 1 < n);
     const bool ok_d = (ri[4] == 0) || (ri[4] == 1 && ri[3] >= 1 && ri[3] + 1 < n) ||
@@ -717,7 +667,7 @@ int fdcn_session_greeks(fdcn_session* s, int32_t T, const int32_t* kind, const i
   char* h = s->pinned().get(L.size);
   if (!h) return sfail(FDCN_ENOMEM, "hipHostMalloc(%zu) failed", L.size);
   uint64_t* a = (uint64_t*)(h + oA);
-  for (int32_t r = 0; r < R; ++r) a[r] = (uint64_t)s->slot_ptr[slots[r]];
+  for (int32_t r = 0; r < R; ++r) a[r] = (uint64_t)s->slots.ptr[slots[r]];
   memcpy(h + oRI, rint, sizeof(int32_t) * R * FDCN_GK_NRINT);
   memcpy(h + oRD, rdbl, sizeof(double) * R * FDCN_GK_NRDBL);
   memcpy(h + oK, kind, sizeof(int32_t) * T);
@@ -757,7 +707,7 @@ int fdcn_session_fetch(fdcn_session* s, int32_t n, const int32_t* slots, int32_t
   char* h = s->pinned().get(L.size);
   if (!h) return sfail(FDCN_ENOMEM, "hipHostMalloc(%zu) failed", L.size);
   uint64_t* a = (uint64_t*)(h + oA);
-  for (int32_t i = 0; i < n; ++i) a[i] = (uint64_t)s->slot_ptr[slots[i]];
+  for (int32_t i = 0; i < n; ++i) a[i] = (uint64_t)s->slots.ptr[slots[i]];
   hipStream_t st;
   if ((rc = pick_stream(s, &st))) return rc;
   if ((rc = wait_producers(s, st, n, slots))) return rc;

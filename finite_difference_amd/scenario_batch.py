@@ -71,19 +71,48 @@ def _num_col(cols: Dict[str, Sequence], key: str, R: int) -> np.ndarray:
         return np.array([np.nan if _missing(v) else float(v) for v in c], np.float64)
 
 
-def _black76(S, K, sigma, t_exp, carry, t_carry, r, t_disc, pv, call):
+def _factorize(col) -> tuple:
+    """(distinct values, index of each row's value) of a column; pandas'
+    hash factorisation when every cell is a value, else the sorted unique
+    strings (str() of every cell, NaN included, as the facade's str(b))."""
+    try:
+        import pandas as pd
+        codes, uniq = pd.factorize(np.asarray(col, dtype=object))
+        if len(codes) and codes.min() >= 0:
+            return list(uniq), np.asarray(codes, np.int64)
+    except ImportError:  # pragma: no cover - pandas ships with the runner
+        pass
+    u, inv = np.unique(np.asarray([str(b) for b in col]), return_inverse=True)
+    return u.tolist(), inv
+
+
+def _black76(S, K, sigma, t_exp, carry, t_carry, r, t_disc, pv, call, shared=None):
     """_vanilla_black76_price (:648-692) elementwise, same operation order;
     math.exp / math.log through libm (capi.vmath), math.sqrt = np.sqrt
-    (both correctly rounded), norm.cdf = scipy.special.ndtr."""
+    (both correctly rounded), norm.cdf = scipy.special.ndtr.  ``shared``
+    (a dict, optional) caches the subexpressions that repeat across the
+    Greeks' repricings -- exp(carry t_carry), exp(-r t_disc), sqrt(t_exp)
+    and log(F / K) per distinct input -- each computed by the same
+    expression on the same operands, so the values are unchanged."""
     from scipy.special import ndtr
+    if shared is None:
+        shared = {}
     S = S - pv
     with np.errstate(all="ignore"):
-        sqrtT = np.sqrt(t_exp)
-        F = S * capi.vmath(capi.VM_EXP, carry * t_carry)
-        d1 = (capi.vmath(capi.VM_LOG, F / K) + (0.5 * sigma * sigma) * t_exp) / (sigma * sqrtT)
+        if ("sqrtT", t_exp) not in shared:
+            shared[("sqrtT", t_exp)] = np.sqrt(t_exp)
+        sqrtT = shared[("sqrtT", t_exp)]
+        if "ec" not in shared:
+            shared["ec"] = capi.vmath(capi.VM_EXP, carry * t_carry)
+            shared["disc"] = capi.vmath(capi.VM_EXP, -r * t_disc)
+        F = S * shared["ec"]
+        key = ("lfk", S.tobytes()) if isinstance(S, np.ndarray) else ("lfk", S)
+        if key not in shared:
+            shared[key] = capi.vmath(capi.VM_LOG, F / K)
+        d1 = (shared[key] + (0.5 * sigma * sigma) * t_exp) / (sigma * sqrtT)
         d2 = d1 - sigma * sqrtT
         Nd1, Nd2 = ndtr(d1), ndtr(d2)
-        disc = capi.vmath(capi.VM_EXP, -r * t_disc)
+        disc = shared["disc"]
         val = (disc * (F * Nd1 - K * Nd2) if call
                else disc * (K * (1.0 - Nd2) - F * (1.0 - Nd1)))
     intr = (t_disc <= 0) | (sigma <= 0)
@@ -95,9 +124,13 @@ def _black76(S, K, sigma, t_exp, carry, t_carry, r, t_disc, pv, call):
 
 def _black76_greeks(S0, K, sig0, T0: float, carry, t_carry: float, r, t_disc: float, pv, call,
                     dS=0.0001, dSigma=0.0001, dT=0.0001) -> Dict[str, np.ndarray]:
-    """_vanilla_black76_greeks_fd (:694-745) elementwise."""
+    """_vanilla_black76_greeks_fd (:694-745) elementwise; the six repricings
+    share exp(carry t_carry), the discount factor, sqrt(T) and log(F / K)
+    where their inputs agree (_black76's ``shared``)."""
+    shared: Dict[Any, np.ndarray] = {}
+
     def price(S=S0, sigma=sig0, T=T0):
-        return _black76(S, K, sigma, T, carry, t_carry, r, t_disc, pv, call)
+        return _black76(S, K, sigma, T, carry, t_carry, r, t_disc, pv, call, shared)
     h = S0 * dS
     p0 = price()
     pu = price(S=S0 + h)
@@ -194,9 +227,11 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
     K = np.asarray(cols["K"], np.float64)
     sig = np.asarray(cols["sigma"], np.float64)
     rate = np.asarray(cols["rate"], np.float64).reshape(R)
-    # barrier kinds through the distinct strings of the column
-    ub, binv = np.unique(np.asarray([str(b) for b in cols["barrier_type"]]), return_inverse=True)
-    bts_u = [b.lower() for b in ub.tolist()]
+    # barrier kinds through the distinct values of the column (a hash
+    # factorisation; str() / lower() per distinct value, as the facade does
+    # per row)
+    ub, binv = _factorize(cols["barrier_type"])
+    bts_u = [str(b).lower() for b in ub]
     ups = _num_col(cols, "upper_barrier", R)
     los = _num_col(cols, "lower_barrier", R)
     if np.any(~(S0 > 0)) or np.any(~(K > 0)) or np.any(~(sig > 0)):
@@ -301,7 +336,8 @@ def result_columns(cols: Dict[str, Sequence], res: Dict[str, np.ndarray]) -> Dic
     R = len(cols["S0"])
     out: Dict[str, Any] = {}
     for k in ("scenario_name", "S0", "K", "sigma", "rate", "barrier_type"):
-        out[k] = list(cols[k])
+        c = cols[k]
+        out[k] = c if isinstance(c, np.ndarray) else list(c)  # arrays stay arrays
     for k in ("upper_barrier", "lower_barrier"):
         out[k] = _num_col(cols, k, R)
     for name in ("price", "delta", "gamma", "vega"):

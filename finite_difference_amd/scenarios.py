@@ -236,7 +236,8 @@ def run_all_scenarios(config_csv_path: str, output_csv_path: Optional[str],
         distributed.bind_device()  # this rank's GPU, before any launch
     mine = distributed.shard_range(len(cfg))
     part = cfg.iloc[mine.start:mine.stop]
-    cols = {k: part[k].tolist() for k in scenario_batch.ROW_KEYS if k in part.columns}
+    # the columns as NumPy arrays: the whole-file path converts nothing per row
+    cols = {k: part[k].to_numpy() for k in scenario_batch.ROW_KEYS if k in part.columns}
     priced = scenario_batch.price_columns(cols, base_params, engine)
     if priced is not None:
         out = scenario_batch.result_columns(cols, priced)

@@ -41,6 +41,20 @@ int fdcn_forced_variant(int32_t* waves, int32_t* npt, int32_t* flavour);
 int fdcn_variant_name(int32_t B, int32_t n_nodes, int32_t it_mode, int32_t k_cap, char* buf,
                       int32_t len);
 
+/* Spot-space march (fdcn_vc_batch[_dev]): pin the compiled variant
+ * (waves, npt) for every subsequent launch it fits, and/or make every
+ * scenario take the stencil form (stencil_only != 0) instead of the
+ * pointwise form the factor kernel would choose.  (0, 0, 0) clears both. */
+int fdcn_vc_force_variant(int32_t waves, int32_t npt, int32_t stencil_only);
+
+/* "fdcn_vc_march<W,NPT>" a spot-space launch of B scenarios runs. */
+int fdcn_vc_variant_name(int32_t B, int32_t n_nodes, char* buf, int32_t len);
+
+/* The form each of B scenarios takes (1 pointwise, 0 stencil): the factor
+ * kernel's classification of diag [B][2][6][n_nodes], run on the host. */
+int fdcn_vc_forms(int32_t B, int32_t n_nodes, int32_t n_time, int32_t n_ranna,
+                  const double* diag, int32_t* form);
+
 #ifdef __cplusplus
 }
 #endif

@@ -80,12 +80,24 @@ def test_paired_flavour_random_batch_vs_oracle():
     assert worst <= TOL
 
 
+@pytest.mark.parametrize("form", ["auto", "stencil"])
 @pytest.mark.parametrize("seed", range(16))
-def test_random_spot_space_pricer_vs_oracle(seed):
+def test_random_spot_space_pricer_vs_oracle(seed, form):
     """fdcn_vc (the spot-space per-row CN of DiscreteBarrierFDMPricer2) on
     seeded random trades: grid 6-3000 nodes, 5-200 steps, every barrier
     type, weekly or no monitoring, the corrected explicit sign (the
-    reference's sign diverges, see test_spot_barrier.py)."""
+    reference's sign diverges, see test_spot_barrier.py).  "auto": the
+    pointwise form these trades classify into; "stencil": every scenario
+    forced onto the stencil form (include/fdcn_diag.h)."""
+    from finite_difference_amd import capi
+    capi.vc_force_variant(0, 0, form == "stencil")
+    try:
+        _spot_space_trade(seed, form)
+    finally:
+        capi.vc_force_variant(0, 0, False)
+
+
+def _spot_space_trade(seed, form):
     import datetime as dt
     from backends import oracle_engine
     from finite_difference_amd.spot_barrier import DiscreteBarrierFDMPricer2
@@ -106,11 +118,16 @@ def test_random_spot_space_pricer_vs_oracle(seed):
         flat_rate_nacc=float(rng.uniform(0.0, 0.08)), num_space_nodes=n, num_time_steps=m,
         engine=Engine(), explicit_sign="corrected")
     _, _, solves = p._grid_solves()
+    from finite_difference_amd import capi
+    from finite_difference_amd.engine import pack_vc
+    g = pack_vc(solves, list(range(len(solves))))
+    forms = capi.vc_forms(g.n_nodes, g.n_time, g.n_ranna, g.diag)
+    assert np.all(forms == (1 if form == "auto" else 0)), forms
     gpu = Engine().run_vc(solves)
     ref = oracle_engine().run_vc(solves)
     worst = max(float(np.max(np.abs(g - r))) / max(1.0, float(np.max(np.abs(r))))
                 for g, r in zip(gpu, ref))
-    print(f"[fuzz vc {seed}] n={n} m={m} {bt} monitored={weekly is not None} "
+    print(f"[fuzz vc {seed} {form}] n={n} m={m} {bt} monitored={weekly is not None} "
           f"solves={len(solves)} worst={worst:.2e}")
     assert worst <= TOL * max(1.0, n / 2048)
 

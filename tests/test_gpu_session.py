@@ -264,3 +264,57 @@ def test_vectorized_american_file_equals_per_row_device(divs):
             g = p.greeks_log2()
             for k in ("price", "delta", "gamma", "vega", "theta"):
                 assert res[k][i] == g[k], (opt, i, k, res[k][i], g[k])
+
+
+def test_destroy_drains_cross_stream_consumers_before_freeing():
+    """ADVICE r2 (medium) / VERDICT r3 item 6: a slot produced on one session
+    stream and read by a launch on another.  The session's fifth and sixth
+    calls round-robin onto streams 0 and 1: the consumer march (v_init from
+    the producer's slots, stream 1) is queued behind a long independent march
+    (stream 1), while the producer's block was allocated on stream 0.
+    fdcn_session_destroy must drain every stream before its stream-ordered
+    frees (else the producer's block returns to the pool while the consumer
+    has not read it yet): destroy takes at least the long march's time.  A
+    new session on the same thread then allocates (from the same pool) and
+    re-runs producer + consumer; its output equals the oracle's two chained
+    segments."""
+    import copy
+    import time
+    from backends import oracle_engine
+    rng = np.random.default_rng(77)
+    n, steps = 1024, 60
+    prod = [random_solve(rng, n, steps, 2, it=False) for _ in range(8)]
+    cons = [copy.copy(s) for s in prod]
+    for c in cons:
+        c.n_ranna = 0
+    small = [random_solve(rng, 513, 20, 2, it=False) for _ in range(4)]
+    long_one = random_solve(rng, 2049, 32768, 2, it=True)  # ~45 ms
+    longs = [long_one] * 2048
+    e = Engine()
+    with Session() as S:  # the long march alone, fetched (its own time)
+        t0 = time.perf_counter()
+        sl = e.march_slots(S, longs)
+        S.fetch(sl[:1], 2049)
+        t_long = time.perf_counter() - t0
+    S = Session()
+    a = e.march_slots(S, prod)          # call 1: stream 0 (producer)
+    e.march_slots(S, longs)             # call 2: stream 1 (long)
+    e.march_slots(S, small[:2])         # call 3: stream 2
+    e.march_slots(S, small[2:])         # call 4: stream 3
+    e.march_slots(S, small[:1])         # call 5: stream 0
+    e.march_slots(S, cons, list(a))     # call 6: stream 1, behind the long march
+    t0 = time.perf_counter()
+    S.close()
+    t_destroy = time.perf_counter() - t0
+    assert t_destroy >= 0.4 * t_long, (t_destroy, t_long)
+    with Session() as S2:
+        a2 = e.march_slots(S2, prod)
+        b2 = e.march_slots(S2, cons, list(a2))
+        got = S2.fetch(b2, n)
+    o = oracle_engine()
+    mid = o.run(prod)
+    for c, v in zip(cons, mid):
+        c.v_init = v
+    want = o.run(cons)
+    for g, w in zip(got, want):
+        assert np.max(np.abs(g - w)) <= 1e-10 * max(1.0, np.max(np.abs(w)))

@@ -86,3 +86,36 @@ def test_timed_instances_are_the_throughput_variants():
     assert capi.variant_name(2049, True, B=4096) == "fdcn_march<1,1,32,0>"
     assert capi.variant_name(1024, False, B=10000) == "fdcn_march<0,1,16,0>"
     assert capi.variant_name(4097, False, B=2048) == "fdcn_march<0,1,64,0>"
+
+
+def test_bench_spot_vc_kernel_vs_oracle_full_length():
+    """bench.py --workload spot_vc times fdcn_vc_march<1,16> on 4 096
+    Pricer2 knock-outs (1 025 nodes, 2 000 steps); every one of its trades
+    takes the pointwise form.  A sample of the bench's own trades on that
+    instance (pinned: a small batch would take shorter chunks), at full
+    length, every node vs the C oracle (oracle_vc_batch, the reference's
+    per-step Thomas, discrete_barrier_fdm_pricer_2.py:336-428)."""
+    from oracle import oracle
+    B = bench.DEFAULT_BATCH["spot_vc"]
+    full = bench.build_spot_vc(24, 1024, 2000)
+    timed = capi.vc_variant_name(full.n_nodes, B=B)
+    assert timed == "fdcn_vc_march<1,16>"
+    assert np.all(capi.vc_forms(full.n_nodes, full.n_time, full.n_ranna, full.diag) == 1)
+    p = capi.vc_plan(full.n_nodes, B=B)
+    capi.vc_force_variant(p["waves"], p["npt"], False)
+    try:
+        assert capi.vc_variant_name(full.n_nodes, B=full.B) == timed
+        got = _gpu_vc(full)
+    finally:
+        capi.vc_force_variant(0, 0, False)
+    ref = oracle.vc_batch(full.n_nodes, full.n_time, full.n_ranna, full.diag, full.bnd,
+                          full.v_init, full.iparams, full.mon_step, full.mon_rebate, 16)
+    scale = np.maximum(1.0, np.max(np.abs(ref), axis=1))
+    rel = np.max(np.abs(got - ref), axis=1) / scale
+    print(f"[spot_vc {timed} {full.n_nodes}x{full.n_time} B={full.B}] max_rel_err={rel.max():.3e}")
+    assert rel.max() <= TOL, rel
+
+
+def _gpu_vc(g):
+    from finite_difference_amd.engine import HipBackend
+    return HipBackend().run_vc_group(g)

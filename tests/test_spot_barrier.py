@@ -218,3 +218,94 @@ def test_spot_dev_entry_skips_repeated_monitor_steps(n):
         assert float(np.max(np.abs(got[b] - ref[b]))) / scale <= 1e-10, b
     # the last projection of each run took effect: knocked-out nodes hold its rebate
     assert got[0][0] == 0.25 * 9 and got[1][-1] == 0.25 * 7
+
+
+def _vanilla_solve(n, m, opt="put"):
+    inp = dict(spot=100.0, strike=100.0, volatility=0.25, option_type=opt, barrier_type="none",
+               flat_rate_nacc=0.05, num_space_nodes=n - 1, num_time_steps=m)
+    return make(inp, None, explicit_sign="corrected")._grid_solves()[2][0]
+
+
+def _with_exceptional_rows(sv, i1, ko=True):
+    """A copy of a vanilla spot-space solve whose CN-phase explicit rows i1
+    and i1 + 1 are no longer -1 times the implicit ones (as the reference's
+    one-sided barrier rows are not, :388-410) -- perturbed by 0.1 %, not
+    flipped: a flipped row in the middle of the grid makes the march grow
+    like 1e53 in 60 steps, and the comparison would measure that growth --
+    with a knock-out below node n/4 and above 3n/4 on every fifth step."""
+    import dataclasses
+    D = sv.diag.copy()
+    for i in (i1, i1 + 1):
+        D[1, 3, i] *= 1.001
+        D[1, 5, i] *= 0.999
+    n = sv.n_nodes
+    kw = dict(ko_lo=n // 4, ko_hi=3 * n // 4, mon_steps=list(range(5, sv.n_time + 1, 5)),
+              mon_rebates=[0.5] * len(range(5, sv.n_time + 1, 5))) if ko else {}
+    return dataclasses.replace(sv, diag=D, **kw)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,npt,n", [(1, 16, 1025), (1, 8, 513), (1, 4, 257), (4, 16, 4097),
+                                     (4, 8, 2049), (16, 4, 4096), (1, 16, 1000)])
+def test_pointwise_exceptional_rows_at_every_slot_position(w, npt, n):
+    """The pointwise form's exceptional rows (csrc/fdcn_vc.hip) at slot 0,
+    1, NPT-2 and NPT-1 of a lane, across a lane and a wave boundary, next to
+    both Dirichlet rows, in the N + 1 layout (node 0 outside the slots) and
+    a padded one, every compiled width: one launch of all positions on the
+    pinned variant, each scenario classified pointwise (asserted) and equal
+    to the oracle; the same launch forced onto the stencil form too."""
+    from finite_difference_amd import capi
+    base = _vanilla_solve(n, 60)
+    slots = 64 * w * npt
+    pad = (slots - n) // 2 if slots >= n else -1
+    lane_edges = [s - pad for s in (npt, npt + 1, 2 * npt - 2, 2 * npt - 1, 64 * npt - 1)]
+    pos = sorted({1, 2, n // 2, n - 3} | {i for i in lane_edges if 1 <= i <= n - 3})
+    solves = [_with_exceptional_rows(base, i) for i in pos] + [base]
+    from finite_difference_amd.engine import pack_vc
+    g = pack_vc(solves, list(range(len(solves))))
+    assert np.all(capi.vc_forms(g.n_nodes, g.n_time, g.n_ranna, g.diag) == 1)
+    ref = oracle_engine().run_vc(solves)
+    try:
+        for stencil in (False, True):
+            capi.vc_force_variant(w, npt, stencil)
+            assert capi.vc_variant_name(n, B=len(solves)) == f"fdcn_vc_march<{w},{npt}>"
+            got = Engine().run_vc(solves)
+            for i, (a, b) in zip(pos + [-1], zip(got, ref)):
+                err = float(np.max(np.abs(a - b))) / max(1.0, float(np.max(np.abs(b))))
+                assert err <= 1e-10, (stencil, i, err)
+    finally:
+        capi.vc_force_variant(0, 0, False)
+
+
+@pytest.mark.gpu
+def test_mixed_forms_in_one_launch():
+    """One launch whose scenarios take different forms: both march kernels
+    run, each on the scenarios the factor kernel gave it -- a corrected
+    Pricer2 knock-out (pointwise, two exceptional rows), a vanilla
+    (pointwise, none), the reference's explicit sign (pointwise, alpha = +1)
+    and a scenario with three scattered exceptional rows (stencil)."""
+    import dataclasses
+    from finite_difference_amd import capi
+    from finite_difference_amd.engine import pack_vc
+    n, m = 1025, 120
+    weekly = [(V0 + dt.timedelta(days=7 * i)).isoformat() for i in range(1, 27)]
+    ko = make(dict(spot=100.0, strike=100.0, volatility=0.25, option_type="call",
+                   barrier_type="up-and-out", upper_barrier=125.0, monitoring_dates=weekly,
+                   flat_rate_nacc=0.05, num_space_nodes=n - 1, num_time_steps=m), None,
+              explicit_sign="corrected")._grid_solves()[2][0]
+    van = _vanilla_solve(n, m, "call")
+    refsign = make(dict(spot=100.0, strike=100.0, volatility=0.25, option_type="put",
+                        barrier_type="none", flat_rate_nacc=0.05, num_space_nodes=n - 1,
+                        num_time_steps=m), None)._grid_solves()[2][0]
+    D = van.diag.copy()
+    for i in (100, 400, 800):
+        D[1, 3, i] *= 1.001
+    odd = dataclasses.replace(van, diag=D)
+    solves = [ko, van, refsign, odd]
+    g = pack_vc(solves, list(range(4)))
+    assert capi.vc_forms(g.n_nodes, g.n_time, g.n_ranna, g.diag).tolist() == [1, 1, 1, 0]
+    got = Engine().run_vc(solves)
+    ref = oracle_engine().run_vc(solves)
+    for k, (a, b) in enumerate(zip(got, ref)):
+        scale = max(1.0, float(np.max(np.abs(b))))
+        assert float(np.max(np.abs(a - b))) / scale <= (1e-9 if k == 2 else 1e-10), k
