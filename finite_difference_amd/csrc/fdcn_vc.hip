@@ -111,6 +111,16 @@ __device__ __forceinline__ double dpp64(double x) {
   return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 constexpr int kRowShr = 0x110, kRowShl = 0x100, kRowBcast15 = 0x142, kRowBcast31 = 0x143;
+// 64-bit DPP move whose lanes without a source keep `old` (bound_ctrl off):
+// wave_shr:1 with old = the carry gives lane 0 the carry without a select
+template <int CTRL>
+__device__ __forceinline__ double dpp64_old(double old, double x) {
+  const unsigned long long o = __double_as_longlong(old), b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffull), (int)(b & 0xffffffffull),
+                                             CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
 
 constexpr int kNC = 5;  // per-slot coefficient arrays: A, B, C, f, e (stencil form);
                         // the pointwise form uses B := g (b - alpha main), f, e
@@ -403,6 +413,9 @@ __global__ void __launch_bounds__(64 * W, (W == 1 && (PW || NPT == 16)) ? 2 : 1)
   // the twelve lane-scan weights of the phase, [wave][weight][lane]: read
   // from LDS in the step (24 VGPRs fewer; the scans are not LDS-bound)
   __shared__ double swt[W * 12 * 64];
+  // the current 64-step block of Dirichlet values, one row per wave: read
+  // back as one LDS broadcast per step instead of four v_readlane
+  __shared__ double2 bblk[W * 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int lane4 = lane << 2;
   asm volatile("" : "+v"(lane4));
@@ -565,16 +578,17 @@ __global__ void __launch_bounds__(64 * W, (W == 1 && (PW || NPT == 16)) ? 2 : 1)
   double next_reb = mpos < mend ? uni(A.mon_rebate[mpos]) : 0.0;
 
   const double2* bnd = reinterpret_cast<const double2*>(A.bnd) + (size_t)scen * A.n_time;
-  double2 bcur = make_double2(0.0, 0.0);
+  const unsigned bb_a = lds_addr(reinterpret_cast<const double*>(bblk + wave * 64));
   // one step; the march runs it in two loops (Rannacher phase, then CN) so
   // the phase switch is not a branch in the step -- inside it the compiler
   // if-converted the whole coefficient reload into every step
   auto step = [&](int m, dvec<NPT>& V, dvec<NPT>& R) __attribute__((always_inline)) {
     if ((m & 63) == 0) {
       const int mm = m + lane;
-      bcur = mm < A.n_time ? bnd[mm] : make_double2(0.0, 0.0);
+      bblk[wave * 64 + lane] = mm < A.n_time ? bnd[mm] : make_double2(0.0, 0.0);
     }
-    const double lo = read_lane(bcur.x, m & 63), hi = read_lane(bcur.y, m & 63);
+    const unsigned ba = hide_addr(bb_a);
+    const double lo = lds_ld(ba, 2 * (m & 63)), hi = lds_ld(ba, 2 * (m & 63) + 1);
 
     double cw, cwb;  // carries into wave 0 (bottom) and the last wave (top)
     if constexpr (PW) {
@@ -654,8 +668,10 @@ __global__ void __launch_bounds__(64 * W, (W == 1 && (PW || NPT == 16)) ? 2 : 1)
     a = fma(lds_ld(sa, 64), dpp64<kRowShr + 2, 0xF>(a), a);
     a = fma(lds_ld(sa, 128), dpp64<kRowShr + 4, 0xF>(a), a);
     a = fma(lds_ld(sa, 192), dpp64<kRowShr + 8, 0xF>(a), a);
-    a = fma(lds_ld(sa, 512), dpp64<kRowBcast15, 0xA>(a), a);
-    a = fma(lds_ld(sa, 576), dpp64<kRowBcast31, 0xC>(a), a);
+    // the row broadcasts write every row (their weights are 0 on the rows
+    // they do not feed): no zeroed destination to prepare
+    a = fma(lds_ld(sa, 512), dpp64<kRowBcast15, 0xF>(a), a);
+    a = fma(lds_ld(sa, 576), dpp64<kRowBcast31, 0xF>(a), a);
     if constexpr (W > 1) {
       if (lane == 63) xch[2 * W + wave] = a;
       __syncthreads();
@@ -664,8 +680,7 @@ __global__ void __launch_bounds__(64 * W, (W == 1 && (PW || NPT == 16)) ? 2 : 1)
         if (v < wave) cw = fma(xch[3 * W + v], cw, xch[2 * W + v]);
     }
     a = fma(Fpre, cw, a);
-    double c = from_below(a, 1, lane4);
-    if (lane == 0) c = cw;
+    double c = dpp64_old<0x138>(cw, a);  // wave_shr:1; lane 0 keeps the carry
     if (lo_out && !PW) v0 = uni(g0 * lo);  // x_0 of this step: cw of wave 0
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
@@ -702,32 +717,28 @@ __global__ void __launch_bounds__(64 * W, (W == 1 && (PW || NPT == 16)) ? 2 : 1)
         if (v > wave) cwb = fma(xch[5 * W + v], cwb, xch[4 * W + v]);
     }
     b = fma(Gsuf, cwb, b);
-    double cb = from_above(b, 1, lane4);
-    if (lane == 63) cb = cwb;
+    double cb = dpp64_old<0x130>(cwb, b);  // wave_shl:1; lane 63 keeps the carry
 #pragma unroll
     for (int k = NPT - 1; k >= 0; --k) {
       cb = fma(ce[k], cb, R[k]);
       R[k] = PW ? fma(alpha, V[k], cb) : cb;  // x = alpha V + u
     }
     if constexpr (PW) {
-      v0 = uni(g0 * lo);  // the Dirichlet rows' x of this step
-      vN = uni(gN * hi);
+      v0 = g0 * lo;  // the Dirichlet rows' x of this step (uniform; left in VGPRs)
+      vN = gN * hi;
     }
 
     // ---- knock-out projection on monitoring steps --------------------------
     if (m + 1 == next_mon) {
       double reb = next_reb;
-      asm volatile("" : "+v"(reb));  // a VGPR copy: v_cndmask takes the mask as its SGPR operand
-      const unsigned rlo = (unsigned)__double_as_longlong(reb);
-      const unsigned rhi = (unsigned)(__double_as_longlong(reb) >> 32);
+      asm volatile("" : "+v"(reb));  // a VGPR copy: the masked move reads it
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) {  // two v_cndmask per slot with the lane mask in SGPRs
-        unsigned lo32 = (unsigned)__double_as_longlong(R[k]);
-        unsigned hi32 = (unsigned)(__double_as_longlong(R[k]) >> 32);
-        asm volatile("v_cndmask_b32 %0, %0, %2, %4\n\tv_cndmask_b32 %1, %1, %3, %4"
-                     : "+v"(lo32), "+v"(hi32)
-                     : "v"(rlo), "v"(rhi), "s"(km[k]));
-        R[k] = __longlong_as_double(((long long)hi32 << 32) | lo32);
+      for (int k = 0; k < NPT; ++k) {  // one v_mov_b64 per slot under the slot's lane mask
+        unsigned long long sv;
+        asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %2\n\tv_mov_b64 %0, %3\n\t"
+                     "s_mov_b64 exec, %1"
+                     : "+v"(R[k]), "=&s"(sv)
+                     : "s"(km[k]), "v"(reb));
       }
       if ((lo_out || PW) && ko0) v0 = reb;
       if (PW && koN) vN = reb;
