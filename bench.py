@@ -218,9 +218,14 @@ def node_units(group) -> int:
 # ---------------------------------------------------------------------------
 # counters measured by tools/pmc_*.sh for THIS kernel source
 # ---------------------------------------------------------------------------
-def kernel_src_sha() -> str:
-    with open(KERNEL_SRC, "rb") as f:
+def file_sha(name: str) -> str:
+    """sha256 prefix of a kernel source file in finite_difference_amd/csrc/."""
+    with open(os.path.join(os.path.dirname(KERNEL_SRC), name), "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def kernel_src_sha() -> str:
+    return file_sha(os.path.basename(KERNEL_SRC))
 
 
 def load_counters(workload: str):
@@ -1008,6 +1013,16 @@ def bench_spot_vc(args):
     tf = fps * node_steps / (kernel_ms * 1e-3) / 1e12
     gbs = BYTES_PER_NODE_STEP[False] * node_steps / (kernel_ms * 1e-3) / 1e9
     slots = 64 * plan["waves"] * plan["npt"]
+    # PMC of this workload (profiles/pmc_counters.json), only if measured on
+    # the current fdcn_vc.hip
+    ctr = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_counters.json")) as f:
+            rec = json.load(f).get(f"spot_vc_{n_space}x{n_time}_batch{g.B}")
+        if rec and rec.get("kernel_src_sha") == file_sha("fdcn_vc.hip"):
+            ctr = rec
+    except (OSError, ValueError):
+        pass
     print(json.dumps({
         "metric": "spot-space CN grid-node-steps/sec/GPU (DiscreteBarrierFDMPricer2 march)",
         "value": node_steps * args.steps / elapsed, "unit": "node-steps/s", "n_gpus": 1,
@@ -1019,8 +1034,15 @@ def bench_spot_vc(args):
                    "grid": [n_space, n_time], "n_nodes": g.n_nodes, "rannacher_steps": 2,
                    "explicit_sign": "corrected"},
         "roofline": {"bound": "fp64_valu", "achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": tf / FP64_VALU_PEAK_TFLOPS, "traffic": None,
+                     "unit": "TFLOP/s", "frac": tf / FP64_VALU_PEAK_TFLOPS,
+                     "traffic": (ctr["march"]["hbm_bytes_per_launch"]
+                                 + ctr["factor"]["hbm_bytes_per_launch"]) if ctr else None,
                      "flops_per_node_step": fps},
+        "valu_issue": ({"march_valu_insts_per_lane_node_step":
+                        ctr["march"]["valu_insts_per_lane_node_step"],
+                        "march_issue_frac": ctr["march"]["valu_issue_utilisation"],
+                        "note": "profiles/pmc_counters.json, measured on this fdcn_vc.hip"}
+                       if ctr else None),
         "roofline_hbm_effective": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "bytes_per_node_step": BYTES_PER_NODE_STEP[False]},
         "kernel_ms_per_launch": kernel_ms,

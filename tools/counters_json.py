@@ -29,17 +29,18 @@ sys.path.insert(0, ROOT)
 XCD = 8
 
 
-def per_launch(d):
+def per_launch(d, kernel="fdcn_march"):
+    """Average per dispatch of the kernels whose name contains `kernel`."""
     per = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(os.path.join(d, "**", "*_counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if "fdcn_march" not in row["Kernel_Name"]:
+            if kernel not in row["Kernel_Name"]:
                 continue
             k = int(row["Dispatch_Id"])
             per[k][row["Counter_Name"]] += float(row["Counter_Value"])
             per[k]["_ns"] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
     if not per:
-        raise SystemExit(f"no fdcn_march rows under {d}")
+        raise SystemExit(f"no {kernel} rows under {d}")
     acc = defaultdict(list)
     for cs in per.values():
         for c, v in cs.items():
@@ -69,12 +70,62 @@ def expected(wl):
     return key, rd + bnd + ko_row + rec, vec + bnd + ko_row + rec, plan, node_steps
 
 
+def spot_vc(tag, out):
+    """The spot-space march (bench.py --workload spot_vc): the pointwise
+    march kernel (the planner's form for every bench trade) and the factor
+    kernel, each per launch; keyed like the bench line's workload."""
+    import bench
+    import numpy as np
+    from finite_difference_amd import capi
+    base = os.path.join(ROOT, "gpurun_out", f"{tag}_spot_vc")
+    B = bench.DEFAULT_BATCH["spot_vc"]
+    g = bench.build_spot_vc(B, 1024, 2000)
+    plan = capi.vc_plan(g.n_nodes, B=B)
+    name = f"fdcn_vc_march<{plan['waves']}, {plan['npt']}, true>"
+    node_steps = g.B * (g.n_nodes - 1) * g.n_time
+    rec = {}
+    for kern, label in ((name, "march"), ("fdcn_vc_factor", "factor")):
+        fe, n1 = per_launch(os.path.join(base, "fetch"), kern)
+        wr, n2 = per_launch(os.path.join(base, "write"), kern)
+        sq, _ = per_launch(os.path.join(base, "sq"), kern)
+        gr, _ = per_launch(os.path.join(base, "grbm"), kern)
+        clk = gr["GRBM_GUI_ACTIVE"] / XCD / gr["_ns"]
+        rec[label] = {
+            "kernel": kern,
+            "hbm_bytes_per_launch": fe["FETCH_SIZE"] * 2 * 1024 + wr["WRITE_SIZE"] * 1024,
+            "read_bytes": fe["FETCH_SIZE"] * 2 * 1024, "write_bytes": wr["WRITE_SIZE"] * 1024,
+            "valu_insts_per_launch": sq["SQ_INSTS_VALU"],
+            "valu_insts_per_lane_node_step": 64.0 * sq["SQ_INSTS_VALU"] / node_steps,
+            "salu_insts_per_launch": sq.get("SQ_INSTS_SALU"),
+            "lds_insts_per_launch": sq.get("SQ_INSTS_LDS"),
+            "wait_inst_any_per_launch": sq.get("SQ_WAIT_INST_ANY"),
+            "gpu_clock_ghz": clk, "profiled_launch_ms": gr["_ns"] * 1e-6,
+            "valu_issue_utilisation": 4.0 * sq["SQ_INSTS_VALU"] / (
+                gr["GRBM_GUI_ACTIVE"] / XCD * 256 * 4),
+            "launches_averaged": min(n1, n2)}
+    # compulsory: diag [B][2][6][n], bnd [B][n_time][2], v_init, v_out
+    compulsory = (g.diag.nbytes + g.bnd.nbytes + 2 * g.v_init.nbytes)
+    key = f"spot_vc_1024x2000_batch{B}"
+    out[key] = dict(rec, kernel_src_sha=bench.file_sha("fdcn_vc.hip"),
+                    compulsory_bytes_per_launch=compulsory,
+                    source=(f"rocprofv3 --pmc, one counter group per pass, python bench.py "
+                            f"--workload spot_vc --steps 2 --warmup 1 (tools/pmc_counters.sh {tag})"))
+    m = rec["march"]
+    print(f"{key}: march VALU per lane node-step {m['valu_insts_per_lane_node_step']:.2f}, issue "
+          f"{m['valu_issue_utilisation']:.2f} at {m['gpu_clock_ghz']:.2f} GHz, HBM march "
+          f"{m['hbm_bytes_per_launch'] / 1e6:.0f} MB + factor "
+          f"{rec['factor']['hbm_bytes_per_launch'] / 1e6:.0f} MB (compulsory {compulsory / 1e6:.0f})")
+
+
 def main():
     import bench
     tag = sys.argv[1]
     wls = sys.argv[2:] or ["american", "barrier", "double"]
     path = os.path.join(ROOT, "profiles", "pmc_counters.json")
     out = json.load(open(path)) if os.path.exists(path) else {}
+    if "spot_vc" in wls:
+        spot_vc(tag, out)
+        wls = [w for w in wls if w != "spot_vc"]
     for wl in wls:
         base = os.path.join(ROOT, "gpurun_out", f"{tag}_{wl}")
         fe, n1 = per_launch(os.path.join(base, "fetch"))
