@@ -14,7 +14,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --t
 # the driver's smoke check (__graft_entry__.smoke, no build: the tree's .so)
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py > $O/bench_american.json 2> $O/bench_american.err || exit $?
-for wl in barrier double analytic scenario_file american_file trade_cnlog trade_american trade_double; do
+for wl in barrier double analytic spot_vc scenario_file american_file trade_cnlog trade_american trade_double; do
   timeout -k 10 300 python bench.py --workload $wl > $O/bench_$wl.json 2> $O/bench_$wl.err || exit $?
 done
 # BASELINE config 4: one 10 000-scenario batch; the per-rank batch sizes of
@@ -25,11 +25,16 @@ for B in 1250 2500 5000; do
   timeout -k 10 300 python bench.py --workload barrier --batch $B --no-cpu-baseline \
       > $O/bench_barrier_b$B.json 2> $O/bench_barrier_b$B.err || exit $?
 done
-for wl in american barrier double; do
+timeout -k 10 300 python bench.py --workload spot_vc --n-space 600 --n-time 600 \
+    > $O/bench_spot_vc_600.json 2> $O/bench_spot_vc_600.err || exit $?
+# config 4 with N = 2 ranks sharing this GPU over gloo (the N > 1 code path)
+FDCN_SHARE_DEVICE=1 timeout -k 10 300 python bench.py --gpus 2 --workload barrier --total 10000 \
+    --backend gloo > $O/bench_barrier_total_2ranks_gloo.json 2> $O/bench_barrier_total_2ranks_gloo.err || exit $?
+for wl in american barrier double spot_vc; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o $wl -- \
       python3 bench.py --workload $wl --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_$wl.log 2>&1 || exit $?
 done
-bash tools/pmc_counters.sh ${TAG}_pmc american barrier double || exit $?
+bash tools/pmc_counters.sh ${TAG}_pmc american barrier double spot_vc || exit $?
 # the launcher path the driver's scaling run uses (one rank here: one GPU)
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
     --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 1 --no-cpu-baseline \
