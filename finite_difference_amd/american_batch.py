@@ -41,24 +41,25 @@ GREEKS = ("price", "delta", "gamma", "vega", "theta")
 def _jobs(sig: np.ndarray, N: int, nsn: int, h: float):
     """Per row the seven requests of price_log2 + greeks_log2
     (AmericanFDMPricer._device_requests) and their unique (sigma, n_time)
-    jobs, in first-use order (the façade's _device_jobs)."""
-    job_row, job_sig, job_nt, req = [], [], [], []
-    for i, s0 in enumerate(sig.tolist()):
-        reqs = [(s0, N), (s0, 2 * N), (s0 + h, N), (s0 - h, N), (s0 + 2.0 * h, N),
-                (s0 - 2.0 * h, N), (s0, 2 * nsn)]
-        keys: Dict[tuple, int] = {}
-        idx = []
-        for sg, nt in reqs:
-            k = (float(sg), int(nt))
-            if k not in keys:
-                keys[k] = len(job_row)
-                job_row.append(i)
-                job_sig.append(float(sg))
-                job_nt.append(int(nt))
-            idx.append(keys[k])
-        req.append(idx)
-    return (np.asarray(job_row, np.int64), np.asarray(job_sig), np.asarray(job_nt, np.int64),
-            np.asarray(req, np.int64))
+    jobs, in first-use order (the façade's _device_jobs), vectorised over the
+    rows: request j of a row reuses the first request j' <= j with the same
+    (sigma, n_time) -- the façade's dict of keys, as a 7 x 7 comparison."""
+    s0 = np.asarray(sig, np.float64).reshape(-1)
+    R = s0.shape[0]
+    S = np.stack([s0, s0, s0 + h, s0 - h, s0 + 2.0 * h, s0 - 2.0 * h, s0], axis=1)
+    NT = np.array([N, 2 * N, N, N, N, N, 2 * nsn], np.int64)
+    eq = (S[:, :, None] == S[:, None, :]) & (NT[:, None] == NT[None, :])[None, :, :]
+    first = np.argmax(eq, axis=2)  # the first j' with the same key (j itself at worst)
+    new = first == np.arange(7)[None, :]
+    n_new = new.sum(axis=1)
+    base = np.concatenate(([0], np.cumsum(n_new)[:-1]))
+    rank = np.cumsum(new, axis=1) - 1  # a new request's index among its row's new ones
+    job_of = base[:, None] + rank      # valid where new
+    req = np.take_along_axis(job_of, first, axis=1)
+    job_row = np.repeat(np.arange(R, dtype=np.int64), n_new)
+    job_sig = S[new]
+    job_nt = np.broadcast_to(NT, (R, 7))[new]
+    return job_row, job_sig, job_nt.astype(np.int64), req.astype(np.int64)
 
 
 def _interp(s: np.ndarray, v: np.ndarray, s0: float) -> float:
@@ -177,6 +178,13 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
 
     members = {nt: np.nonzero(job_nt == nt)[0] for nt in nts}
     n_seg = max(len(segs[nt][2]) for nt in nts)
+    # per job: its grid's dividend count and each dividend's cash amount
+    nt_ix = np.searchsorted(np.asarray(nts, np.int64), job_nt)
+    n_div = np.array([len(segs[nt][0]) for nt in nts], np.int64)[nt_ix]
+    cash_tab = np.zeros((len(nts), max(1, int(n_div.max(initial=0)))))
+    for a, nt in enumerate(nts):
+        for d, (_, amt) in enumerate(segs[nt][0]):
+            cash_tab[a, d] = amt
     if not host:
         from .session import GK_AMERICAN, Session
         with Session() as S:
@@ -192,10 +200,9 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
                     slot[m] = S.march(g, None if seg == 0 else slot[m])
                     eng.launches += 1
                     eng.solves += len(m)
-                jump = np.array([j for j in range(J) if seg < len(segs[int(job_nt[j])][0])],
-                                np.int64)
+                jump = np.nonzero(seg < n_div)[0]
                 if len(jump):
-                    cash = np.array([segs[int(job_nt[j])][0][seg][1] for j in jump])
+                    cash = cash_tab[nt_ix[jump], seg]
                     kc = plan["gout"][jump, 1] if call else np.full(len(jump), -1.0)
                     slot[jump] = S.dividend_jump(slot[jump], plan["s_nodes"][jump], cash, kc)
             # seven readouts per row: the cubic ones for the N and 2N grids
