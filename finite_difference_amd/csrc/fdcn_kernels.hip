@@ -558,6 +558,11 @@ fdcn_march(KArgs A) {
                (kPair ? 2 * lds_doubles_per_scen<IT, W, NPT, ZG>(lz) - kScanLdsDoubles : 0);
   (void)sw;
   (void)xch;
+  // this lane's column of the scan weights as an LDS byte address the
+  // compiler cannot rematerialise (hide_addr at each use): the two-pass step
+  // reads stages 2-5 off it with immediate offsets
+  const unsigned sw_a = kScanLds ? lds_addr(sw + lane) : 0u;
+  (void)sw_a;
   // this wave's block of boundary terms (kBndLds): after the scan weights
   constexpr bool kBndLds = Geo<IT, W, NPT, ZG>::kBndLds;
   double2* bblk = reinterpret_cast<double2*>(
@@ -595,26 +600,15 @@ fdcn_march(KArgs A) {
   // steps m = hl (mod L) are this lane's (kStride lanes per scenario)
   constexpr int kStride = kPair ? 32 : 64;
   double tau_end = tau0 + (double)A.n_time * dt;  // tau after the last step
-  if (tau_mode == 1) {
-    // (tau_{m+1}, tau_m) of every step into the owner lane's workspace slot
-    // (read back by the same lane below), run by run (tau_next_run)
-    double tc = tau0;
-    int kc = 0;
-    TauRun run;
-    while (tau_next_run(tc, kc, A.n_pad, dt, run)) {  // uniform per scenario
-      if (run.k < A.n_time && A.n_time <= run.k + run.len)
-        tau_end = (A.n_time == run.k + run.len)
-                      ? run.t_next : run.t + (double)(A.n_time - run.k) * run.delta;
-      for (int m = run.k + ((hl - run.k) & (kStride - 1)); m < run.k + run.len && valid;
-           m += kStride) {
-        const int j = m - run.k;
-        const double tp = run.t + (double)j * run.delta;
-        const double tn = (j + 1 == run.len) ? run.t_next : run.t + (double)(j + 1) * run.delta;
-        bnd[m] = make_double2(tn, tp);
-      }
-    }
-    __threadfence_block();
-  }
+  // tau_mode 1: the runs of the tau sequence (tau_next_run) are walked chunk
+  // by chunk below, each lane picking (tau_{m+1}, tau_m) of its own step from
+  // the runs overlapping the chunk -- no round trip of the tau pairs through
+  // the workspace (2 x 16 B per step and scenario: 2 x 268 MB per config-2
+  // launch), and the boundary values' exp stays outside any divergent branch
+  double tc = tau0;
+  int kc = 0;
+  TauRun run;
+  bool have_run = tau_mode == 1 && tau_next_run(tc, kc, A.n_pad, dt, run);
   // Split-form CN (kSplit below) tabulates its rhs terms too: th (-A_L)(lo_new
   // + c2 lo_prev) with lo_prev the previous step's Dirichlet value, the
   // expression and operand order of the in-loop form it replaces (bitwise the
@@ -629,13 +623,25 @@ fdcn_march(KArgs A) {
     const double* vb = A.v_init + (size_t)scen * n_nodes;
     const double v_lo0 = (IT || kTabSplit) ? U(vb[0]) : 0.0;
     const double v_hi0 = (IT || kTabSplit) ? U(vb[n_nodes - 1]) : 0.0;
-    for (int m = hl; m < A.n_pad && valid; m += kStride) {
+    for (int c = 0; c < A.n_pad; c += kStride) {
+      const int m = c + hl;
       double tau = tau0 + (double)(m + 1) * dt, tp = tau0 + (double)m * dt;
-      if (tau_mode == 1) {
-        const double2 tt = bnd[m];
-        tau = tt.x;
-        tp = tt.y;
+      if (tau_mode == 1) {  // uniform per scenario: the runs overlapping [c, c + kStride)
+        for (;;) {
+          if (!have_run) break;
+          if (run.k < A.n_time && A.n_time <= run.k + run.len)
+            tau_end = (A.n_time == run.k + run.len)
+                          ? run.t_next : run.t + (double)(A.n_time - run.k) * run.delta;
+          if (m >= run.k && m < run.k + run.len) {
+            const int j = m - run.k;
+            tp = run.t + (double)j * run.delta;
+            tau = (j + 1 == run.len) ? run.t_next : run.t + (double)(j + 1) * run.delta;
+          }
+          if (run.k + run.len >= c + kStride) break;  // continues into the next chunk
+          have_run = tau_next_run(tc, kc, A.n_pad, dt, run);
+        }
       }
+      if (!valid) continue;
       (void)tp;
       const double lo = bnd_eval(lof, l0, l1, l2, l3, tau), hi = bnd_eval(hif, h0, h1, h2, h3, tau);
       if constexpr (IT) {
@@ -1128,14 +1134,17 @@ fdcn_march(KArgs A) {
     double e = a[0];
 #pragma unroll
     for (int j = 1; j < S; ++j) e = fma(j == S - 1 ? mulLF : fmM, e, a[j]);
-    double b = e;
+    // stage 0 unconditional on the split form: the config-3 grids all need
+    // it, and a conditional stage costs a copy of e (still live in the last
+    // node's register) on the common path
+    double b = kSplit ? fma(FW[0], scan_up(e, 1, lane4), e) : e;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = kSplit ? 1 : 0; j < 2; ++j)
       if (!kSplit || j < nst_f) b = fma(FW[j], scan_up(b, 1 << j, lane4), b);
     if (nst_f > 2) {
 #pragma unroll
       for (int j = 2; j < 6; ++j) {
-        const double wf = kScanLds ? sw[(j - 2) * 128 + lane] : FW[j];
+        const double wf = kScanLds ? lds_ld(hide_addr(sw_a), (j - 2) * 128) : FW[j];
         if (j < nst_f) b = fma(wf, scan_up(b, 1 << j, lane4), b);
       }
     }
@@ -1177,7 +1186,7 @@ fdcn_march(KArgs A) {
     if (nst_b > 2) {
 #pragma unroll
       for (int j = 2; j < 6; ++j) {
-        const double wg = kScanLds ? sw[(j - 2) * 128 + 64 + lane] : GW[j];
+        const double wg = kScanLds ? lds_ld(hide_addr(sw_a), (j - 2) * 128 + 64) : GW[j];
         if (j < nst_b) cb = fma(wg, scan_dn(cb, 1 << j, lane4), cb);
       }
     }
