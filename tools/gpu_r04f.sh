@@ -11,6 +11,7 @@ O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_timed_variants.py \
-    tests/test_gpu_pricers.py tests/test_gpu_boundary.py tests/test_gpu_fuzz.py -m gpu -x -q \
+    tests/test_gpu_pricers.py tests/test_gpu_boundary.py tests/test_gpu_fuzz.py tests/test_spot_barrier.py \
+    tests/test_spot_barrier_analytic.py -m gpu -x -q \
     -p no:cacheprovider --timeout 180 --timeout-method thread > $O/tests.log 2>&1 || exit $?
-bash tools/gpu_ab.sh ${TAG}_ab "c3base c3new" "barrier american double" --steps 10 || exit $?
+bash tools/gpu_ab.sh ${TAG}_ab "c3base c3new" "barrier american double spot_vc" --steps 10 || exit $?
