@@ -181,8 +181,10 @@ def _greeks_host(V: np.ndarray, rint: np.ndarray, rdbl: np.ndarray, tpar: np.nda
 
 
 def _march_and_finish(eng: Engine, plan: dict, n_time: int, n_ranna: int,
-                      mon: np.ndarray) -> np.ndarray:
-    """March the plan's 2R solves as one launch and run the Greeks epilogue."""
+                      mon: np.ndarray, overlap=None) -> np.ndarray:
+    """March the plan's 2R solves as one launch and run the Greeks epilogue.
+    ``overlap`` (optional): host work that does not need the march, run
+    while the device marches (the launch is asynchronous)."""
     Q = plan["params"].shape[0]
     g = Group(False, plan["n_nodes"], n_time, min(n_ranna, n_time), plan["params"],
               plan["iparams"], plan["v_init"], None, np.tile(mon, Q), plan["mon_rebate"],
@@ -194,11 +196,15 @@ def _march_and_finish(eng: Engine, plan: dict, n_time: int, n_ranna: int,
             slots = S.march(g)
             eng.launches += 1
             eng.solves += Q
+            if overlap is not None:
+                overlap()
             RI = RI.copy()
             RI[:, 0] = slots[RI[:, 0]]
             return S.greeks_raw(np.full(Q // 2, GK_BARRIER, np.int32),
                                 np.arange(0, Q, 2, dtype=np.int32), plan["tparams"], RI,
                                 plan["rdbl"])
+    if overlap is not None:
+        overlap()
     V = eng.backend.run_group(g)
     eng.launches += 1
     eng.solves += Q
@@ -267,10 +273,19 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
 
     out = {k: np.zeros(R) for k in GREEKS}
     binv = binv.reshape(R)
+    van = None  # Black-76 legs (vanilla rows, knock-in parity), see below
+    gv: Dict[str, np.ndarray] = {}
+
+    def black76_legs():
+        if van is not None and np.any(van):
+            vi = np.nonzero(van)[0]
+            gv.update(_black76_greeks(S0[vi], K[vi], sig[vi], T, carry[vi], t_carry, disc[vi],
+                                      t_disc, pv[vi], call))
     is_ko = np.array([b in KO_KIND for b in bts_u], bool)[binv]
     kind_u = [KO_KIND[b] if b in KO_KIND and not already_hit else
               KI_KIND[b] if b in KI_KIND and not already_in else 0 for b in bts_u]
     kind = np.asarray(kind_u, np.int32)[binv]
+    van = ~is_ko
     pde = np.nonzero(kind)[0]
     if len(pde):
         Rp = len(pde)
@@ -300,7 +315,9 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
                 return None  # two launch shapes: the per-row path groups them
             raise
         t1 = time.perf_counter()
-        res = _march_and_finish(eng, plan, n_time, int(p0.rannacher_steps), mon)
+        # the Black-76 legs run on the host while the device marches
+        res = _march_and_finish(eng, plan, n_time, int(p0.rannacher_steps), mon,
+                                overlap=black76_legs)
         if timing is not None:
             timing["plan"] = t1 - t0
             timing["march"] = time.perf_counter() - t1
@@ -313,11 +330,10 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
                         for p in per_rate])
         out["price"][is_ko] = reb[rix[is_ko]]
     # Black-76 legs: vanilla rows, knocked-in rows, and knock-in parity
-    van = ~is_ko
     if np.any(van):
         vi = np.nonzero(van)[0]
-        gv = _black76_greeks(S0[vi], K[vi], sig[vi], T, carry[vi], t_carry, disc[vi], t_disc,
-                             pv[vi], call)
+        if not gv:  # no PDE rows: nothing to overlap with
+            black76_legs()
         ki = kind[vi] != 0  # knock-in with a PDE leg: vanilla - knock-out
         for k in GREEKS:
             out[k][vi] = np.where(ki, gv[k] - out[k][vi], gv[k])
