@@ -715,17 +715,18 @@ def bench_scenario_file(args):
         return scenario_batch.result_columns(cols, res)
     for _ in range(args.warmup):
         one({})
-    walls, plans, marches = [], [], []
+    walls, parts = [], {}
     out = None
     for _ in range(args.steps):
         tm = {}
         t0 = time.perf_counter()
         out = one(tm)
         walls.append(time.perf_counter() - t0)
-        plans.append(tm["plan"])
-        marches.append(tm["march"])
+        for k, v in tm.items():
+            parts.setdefault(k, []).append(v)
     ms = sum(walls) / len(walls) * 1e3
-    march_ms = sum(marches) / len(marches) * 1e3
+    avg = {k: sum(v) / len(v) * 1e3 for k, v in parts.items()}
+    march_ms = avg["march"]
     n_pde = sum(1 for b in bt if b != "none")
     print(json.dumps({
         "metric": "scenario file wall time (run_all_scenarios pricing)",
@@ -736,8 +737,8 @@ def bench_scenario_file(args):
                 "barriers; two curves)",
         "config": {"workload": f"scenario_file_{R}rows_{N}x{M}", "config": "BASELINE configs[2]",
                    "rows": R, "pde_rows": n_pde, "solves": 2 * n_pde},
-        "host_ms": ms - march_ms, "plan_ms": sum(plans) / len(plans) * 1e3,
-        "march_and_epilogue_ms": march_ms,
+        "host_ms": ms - march_ms, "plan_ms": avg["plan"], "march_and_epilogue_ms": march_ms,
+        "host_parts_ms": {k: avg[k] for k in ("prep", "plan", "free") if k in avg},
         "outputs_finite": bool(np.all(np.isfinite(out["model_price"])))}), flush=True)
 
 
@@ -767,17 +768,18 @@ def bench_american_file(args):
         return american_batch.result_columns(cols, res)
     for _ in range(args.warmup):
         one({})
-    walls, plans, marches = [], [], []
+    walls, parts = [], {}
     out = None
     for _ in range(args.steps):
         tm = {}
         t0 = time.perf_counter()
         out = one(tm)
         walls.append(time.perf_counter() - t0)
-        plans.append(tm["plan"])
-        marches.append(tm["march"])
+        for k, v in tm.items():
+            parts.setdefault(k, []).append(v)
     ms = sum(walls) / len(walls) * 1e3
-    march_ms = sum(marches) / len(marches) * 1e3
+    avg = {k: sum(v) / len(v) * 1e3 for k, v in parts.items()}
+    march_ms = avg["march"]
     node_steps = R * (5 * N * M + N * 2 * M)  # N, sigma +-h, +-2h at M steps; 2M
     print(json.dumps({
         "metric": "American scenario file wall time (run_all_american_scenarios pricing)",
@@ -788,8 +790,9 @@ def bench_american_file(args):
                 "two curves)",
         "config": {"workload": f"american_file_{R}rows_{N}x{M}", "config": "BASELINE configs[1]",
                    "rows": R, "grids_per_row": 6},
-        "host_ms": ms - march_ms, "plan_ms": sum(plans) / len(plans) * 1e3,
-        "march_and_epilogue_ms": march_ms, "node_steps_per_s": node_steps / (ms * 1e-3),
+        "host_ms": ms - march_ms, "plan_ms": avg["plan"], "march_and_epilogue_ms": march_ms,
+        "host_parts_ms": {k: avg[k] for k in ("prep", "plan", "free") if k in avg},
+        "node_steps_per_s": node_steps / (ms * 1e-3),
         "outputs_finite": bool(np.all(np.isfinite(out["model_price"])))}), flush=True)
 
 

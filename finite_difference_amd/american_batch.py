@@ -28,6 +28,7 @@ per-row runner's exactly.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -126,6 +127,7 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
     import time
     from . import scenarios
     from .american import AmericanFDMPricer
+    t_start = time.perf_counter()
     eng = engine if engine is not None else default_engine()
     R = len(cols["S0"])
     if R == 0:
@@ -153,30 +155,68 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
     t0 = time.perf_counter()
     job_row, job_sig, job_nt, req = _jobs(sig, N, nsn, dv_sigma)
     J = len(job_row)
+    # jobs grouped by step count (stable): each launch's rows are one
+    # contiguous block of the plan arrays, handed over as views
+    perm = np.argsort(job_nt, kind="stable")
+    inv = np.empty(J, np.int64)
+    inv[perm] = np.arange(J)
+    job_row, job_sig, job_nt, req = job_row[perm], job_sig[perm], job_nt[perm], inv[req]
     job = np.stack([spot[job_row], K[job_row], job_sig, carry[job_row], disc[job_row]], axis=1)
     divs = p0._div_times_tau()
     host = not eng.on_device
-    plan = capi.american_plan(job, np.full(J, 1 if call else 0, np.int32), nsn, p0.s_max_mult,
-                              p0.time_to_expiry, with_grids=bool(divs) or host)
+    with contextlib.ExitStack() as stack:
+        S = None
+        if not host:
+            from .session import Session
+            S = stack.enter_context(Session())
+        # on the device the payoffs are written straight into the session's
+        # pinned memory: each launch copies its block from there
+        plan = capi.american_plan(job, np.full(J, 1 if call else 0, np.int32), nsn,
+                                  p0.s_max_mult, p0.time_to_expiry,
+                                  with_grids=bool(divs) or host,
+                                  payoff_out=None if S is None else S.host_buffer)
+        res = _march_plan(eng, S, plan, p0, job_nt, req, spot, sig, carry, disc, dv_sigma,
+                          call, N, nsn, timing, t0)
+        del plan  # the pinned view goes before the session closes
+        t2 = time.perf_counter()
+    if timing is not None:
+        timing["prep"] = t0 - t_start
+        timing["march"] = t2 - timing.pop("_t1")
+        timing["free"] = time.perf_counter() - t2
+    return res
+
+
+def _march_plan(eng: Engine, S, plan: dict, p0, job_nt, req, spot, sig, carry, disc,
+                dv_sigma: float, call: bool, N: int, nsn: int, timing, t0: float):
+    """Every job's segments (lock-step launches per step count, device
+    dividend jumps) and the per-row readouts: on the session S, or through
+    the engine's backend when S is None."""
+    import time
+    J, R = len(job_nt), len(spot)
+    host = S is None
     n1 = nsn + 1
     nts = sorted(set(job_nt.tolist()))
     segs = {nt: p0._segments(nt) for nt in nts}
     t1 = time.perf_counter()
+    if timing is not None:
+        timing["plan"] = t1 - t0
+        timing["_t1"] = t1
 
-    def group(members: np.ndarray, nt: int, seg: int, v_init) -> Group:
+    def group(m: slice, nt: int, seg: int, v_init) -> Group:
         # v_init None: the first segment, which starts from the payoff (one
         # array for both, so a session stages it once)
         _, pts, steps = segs[nt]
-        P = plan["params"][members].copy()
+        P = plan["params"][m].copy()
         P[:, capi.P_DT] = (pts[seg + 1] - pts[seg]) / float(steps[seg])
         P[:, capi.P_TAU0] = pts[seg]
         restart = seg == 0 or call
-        pay = plan["payoff"][members]
+        pay = plan["payoff"][m]
         return Group(True, n1, int(steps[seg]), p0.rannacher_steps if restart else 0, P,
-                     plan["iparams"][members], pay if v_init is None else v_init, pay,
-                     np.zeros(0, np.int32), np.zeros(0), list(members))
+                     plan["iparams"][m], pay if v_init is None else v_init, pay,
+                     np.zeros(0, np.int32), np.zeros(0), list(range(m.start, m.stop)))
 
-    members = {nt: np.nonzero(job_nt == nt)[0] for nt in nts}
+    bounds = np.searchsorted(job_nt, np.asarray(nts, np.int64), side="left").tolist() + [J]
+    members = {nt: slice(bounds[a], bounds[a + 1]) for a, nt in enumerate(nts)}
     n_seg = max(len(segs[nt][2]) for nt in nts)
     # per job: its grid's dividend count and each dividend's cash amount
     nt_ix = np.searchsorted(np.asarray(nts, np.int64), job_nt)
@@ -186,34 +226,33 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
         for d, (_, amt) in enumerate(segs[nt][0]):
             cash_tab[a, d] = amt
     if not host:
-        from .session import GK_AMERICAN, Session
-        with Session() as S:
-            slot = np.full(J, -1, np.int32)
-            for seg in range(n_seg):
-                for nt in nts:
-                    steps = segs[nt][2]
-                    if seg >= len(steps) or steps[seg] < 1:
-                        continue
-                    m = members[nt]
-                    # later segments start from the slots (no host vector)
-                    g = group(m, nt, seg, None if seg == 0 else np.empty((len(m), 0)))
-                    slot[m] = S.march(g, None if seg == 0 else slot[m])
-                    eng.launches += 1
-                    eng.solves += len(m)
-                jump = np.nonzero(seg < n_div)[0]
-                if len(jump):
-                    cash = cash_tab[nt_ix[jump], seg]
-                    kc = plan["gout"][jump, 1] if call else np.full(len(jump), -1.0)
-                    slot[jump] = S.dividend_jump(slot[jump], plan["s_nodes"][jump], cash, kc)
-            # seven readouts per row: the cubic ones for the N and 2N grids
-            cub = np.array([1, 1, 0, 0, 0, 0, 0], np.int64)
-            rows = (2 * req + cub[None, :]).reshape(-1)
-            RI = plan["rint"][rows].copy()
-            RI[:, 0] = slot[RI[:, 0]]
-            tp = np.zeros((R, capi.GK_NPARAM))
-            tp[:, 0], tp[:, 1], tp[:, 2], tp[:, 3], tp[:, 4] = sig, spot, carry, disc, dv_sigma
-            out = S.greeks_raw(np.full(R, GK_AMERICAN, np.int32),
-                               np.arange(0, 7 * R, 7, dtype=np.int32), tp, RI, plan["rdbl"][rows])
+        from .session import GK_AMERICAN
+        slot = np.full(J, -1, np.int32)
+        for seg in range(n_seg):
+            for nt in nts:
+                steps = segs[nt][2]
+                if seg >= len(steps) or steps[seg] < 1:
+                    continue
+                m = members[nt]
+                # later segments start from the slots (no host vector)
+                g = group(m, nt, seg, None if seg == 0 else np.empty((m.stop - m.start, 0)))
+                slot[m] = S.march(g, None if seg == 0 else slot[m])
+                eng.launches += 1
+                eng.solves += m.stop - m.start
+            jump = np.nonzero(seg < n_div)[0]
+            if len(jump):
+                cash = cash_tab[nt_ix[jump], seg]
+                kc = plan["gout"][jump, 1] if call else np.full(len(jump), -1.0)
+                slot[jump] = S.dividend_jump(slot[jump], plan["s_nodes"][jump], cash, kc)
+        # seven readouts per row: the cubic ones for the N and 2N grids
+        cub = np.array([1, 1, 0, 0, 0, 0, 0], np.int64)
+        rows = (2 * req + cub[None, :]).reshape(-1)
+        RI = plan["rint"][rows].copy()
+        RI[:, 0] = slot[RI[:, 0]]
+        tp = np.zeros((R, capi.GK_NPARAM))
+        tp[:, 0], tp[:, 1], tp[:, 2], tp[:, 3], tp[:, 4] = sig, spot, carry, disc, dv_sigma
+        out = S.greeks_raw(np.full(R, GK_AMERICAN, np.int32),
+                           np.arange(0, 7 * R, 7, dtype=np.int32), tp, RI, plan["rdbl"][rows])
         res = {k: out[:, j] for j, k in enumerate(GREEKS)}
         res["price_log2"] = out[:, 5]
     else:
@@ -224,11 +263,11 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
                 if seg >= len(steps) or steps[seg] < 1:
                     continue
                 m = members[nt]
-                v0 = None if seg == 0 else np.stack([V[j] for j in m])
+                v0 = None if seg == 0 else np.stack([V[j] for j in range(m.start, m.stop)])
                 out = eng.backend.run_group(group(m, nt, seg, v0))
                 eng.launches += 1
-                eng.solves += len(m)
-                for r_, j in enumerate(m):
+                eng.solves += m.stop - m.start
+                for r_, j in enumerate(range(m.start, m.stop)):
                     V[j] = out[r_]
             for j in range(J):
                 dv = segs[int(job_nt[j])][0]
@@ -237,9 +276,6 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
                     V[j] = capi.dividend_jump(plan["s_nodes"][j], V[j], dv[seg][1], kc)
         res = _finish_host(V, plan["s_nodes"], plan["gout"][:, 0], req, spot, sig, carry, disc,
                            dv_sigma)
-    if timing is not None:
-        timing["plan"] = t1 - t0
-        timing["march"] = time.perf_counter() - t1
     return res
 
 

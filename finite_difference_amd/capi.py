@@ -39,7 +39,8 @@ EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batc
             "fdcn_double_barrier_batch_dev", "fdcn_last_error", "fdcn_device_count",
             "fdcn_abi_version", "fdcn_select_device", "fdcn_current_device",
             "fdcn_tau_sequence", "fdcn_tau_runs", "fdcn_session_create",
-            "fdcn_session_destroy", "fdcn_session_slots", "fdcn_session_march",
+            "fdcn_session_destroy", "fdcn_session_slots", "fdcn_session_host_buffer",
+            "fdcn_session_march",
             "fdcn_session_dividend_jump", "fdcn_session_greeks", "fdcn_session_fetch",
             "fdcn_vc_batch", "fdcn_vc_batch_dev", "fdcn_vc_plan", "fdcn_barrier_plan",
             "fdcn_vmath", "fdcn_american_plan", "fdcn_device_ordinals")
@@ -442,9 +443,11 @@ AP_NJOB, AP_NOUT = 5, 4    # FDCN_AP_NJOB / FDCN_AP_NOUT
 
 
 def american_plan(job: np.ndarray, call: np.ndarray, n_space: int, s_max_mult: float,
-                  T: float, with_grids: bool = False) -> dict:
+                  T: float, with_grids: bool = False, payoff_out=None) -> dict:
     """fdcn_american_plan: grid, payoff, coefficients and readouts of J
-    American (row, sigma) jobs, host only (see include/fdcn.h)."""
+    American (row, sigma) jobs, host only (see include/fdcn.h).
+    ``payoff_out`` (optional): a callable n -> float64 array of n elements
+    the payoffs are written into (a session's pinned host buffer)."""
     job = np.ascontiguousarray(job, np.float64)
     call = np.ascontiguousarray(call, np.int32)
     J = job.shape[0]
@@ -452,7 +455,8 @@ def american_plan(job: np.ndarray, call: np.ndarray, n_space: int, s_max_mult: f
         raise ValueError("american_plan: job [J, 5] and call [J] expected")
     n1 = int(n_space) + 1
     out = dict(params=np.empty((J, NPARAM)), iparams=np.empty((J, NIPARAM), np.int32),
-               payoff=np.empty((J, n1)), s_nodes=np.empty((J, n1)) if with_grids else None,
+               payoff=(np.empty(J * n1) if payoff_out is None
+                       else payoff_out(J * n1)).reshape(J, n1), s_nodes=np.empty((J, n1)) if with_grids else None,
                rint=np.empty((2 * J, GK_NRINT), np.int32), rdbl=np.empty((2 * J, GK_NRDBL)),
                gout=np.empty((J, AP_NOUT)))
     _check(lib().fdcn_american_plan(
@@ -466,11 +470,13 @@ GK_NPARAM, GK_NRINT, GK_NRDBL = 8, 5, 8
 
 def barrier_plan(row: np.ndarray, flag: np.ndarray, T: float, n_space: int, n_time: int,
                  grid_mode: int, k_tail: float, dv_sigma: float,
-                 rebate_at_hit: bool, mon_k: np.ndarray) -> dict:
+                 rebate_at_hit: bool, mon_k: np.ndarray, v_init_out=None) -> dict:
     """fdcn_barrier_plan: base and sigma-bumped solve of every row (solve
     q = 2 row + bump), host only.  Returns the launch arrays (params, iparams,
     v_init, mon_rebate), the readouts (rint with the solve index in column 0,
-    rdbl), the per-row epilogue parameters and n_nodes."""
+    rdbl), the per-row epilogue parameters and n_nodes.  ``v_init_out``
+    (optional): a callable n -> float64 array of n elements the initial
+    vectors are written into (a session's pinned host buffer)."""
     row = np.ascontiguousarray(row, np.float64)
     flag = np.ascontiguousarray(flag, np.int32)
     R = row.shape[0]
@@ -483,7 +489,8 @@ def barrier_plan(row: np.ndarray, flag: np.ndarray, T: float, n_space: int, n_ti
         n_max = int(n_space)
     Q = 2 * R
     out = dict(params=np.empty((Q, NPARAM)), iparams=np.empty((Q, NIPARAM), np.int32),
-               v_init=np.empty(Q * n_max), mon_rebate=np.empty(max(1, Q * mon.size)),
+               v_init=np.empty(Q * n_max) if v_init_out is None else v_init_out(Q * n_max),
+               mon_rebate=np.empty(max(1, Q * mon.size)),
                rint=np.empty((Q, GK_NRINT), np.int32), rdbl=np.empty((Q, GK_NRDBL)),
                tparams=np.empty((R, GK_NPARAM)))
     nn = np.zeros(1, np.int32)

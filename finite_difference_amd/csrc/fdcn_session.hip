@@ -502,6 +502,13 @@ int fdcn_session_destroy(fdcn_session* s) {
 
 int fdcn_session_slots(const fdcn_session* s) { return s ? (int)s->slots.size() : -1; }
 
+int fdcn_session_host_buffer(fdcn_session* s, int64_t bytes, void** out) {
+  if (!s || !out || bytes < 0) return sfail(FDCN_EINVAL, "fdcn_session_host_buffer: bad argument");
+  *out = s->pinned().get((size_t)bytes);
+  if (!*out) return sfail(FDCN_ENOMEM, "hipHostMalloc(%lld) failed", (long long)bytes);
+  return FDCN_OK;
+}
+
 int fdcn_session_march(fdcn_session* s, int32_t it, int32_t B, int32_t n_nodes, int32_t n_time,
                        int32_t n_ranna, const double* params, const int32_t* iparams,
                        const double* v_init, const int32_t* v_init_slots, const double* payoff,
@@ -525,44 +532,60 @@ int fdcn_session_march(fdcn_session* s, int32_t it, int32_t B, int32_t n_nodes, 
   if ((rc = fdcn_plan(B, n_nodes, n_time, it, k_cap, &w_, &npt_, &spb_, &lds_, &ws_))) return rc;
 
   const size_t nv = (size_t)B * n_nodes, nm = (size_t)(n_mon > 0 ? n_mon : 1);
-  // inputs first (one H2D copy of the staged prefix), then device-only buffers
+  const size_t vb = sizeof(double) * nv;
+  // the small inputs, the payoff and v_init, then device-only buffers
   Layout L;
   const size_t oP = L.add(sizeof(double) * B * FDCN_NPARAM);
   const size_t oI = L.add(sizeof(int32_t) * B * FDCN_NIPARAM);
   const size_t oM = L.add(sizeof(int32_t) * nm);
   const size_t oR = L.add(sizeof(double) * nm);
-  const size_t oF = it ? L.add(sizeof(double) * nv) : 0;
   const size_t oA = v_init_slots ? L.add(sizeof(uint64_t) * B) : 0;
+  const size_t pre = L.size;  // the small inputs: [0, pre)
+  const size_t oF = it ? L.add(vb) : 0;
   // an IT march whose host v_init is its payoff array (the first segment of
-  // an American grid) stages that array once and reads it twice
+  // an American grid) copies that array once and reads it twice
   const bool v_is_payoff = it && v_init && v_init == payoff;
-  const size_t oV = L.add(sizeof(double) * nv);  // staged only for host v_init
-  const size_t staged = (v_init && !v_is_payoff) ? L.size : oV;
-  const size_t oO = L.add(sizeof(double) * nv);
+  const size_t oV = L.add(vb);  // copied only for a host v_init
+  const size_t oO = L.add(vb);
   const size_t ws_bytes = (size_t)ws_ * (size_t)B;
   const size_t oW = L.add(ws_bytes);
+  // A payoff / v_init inside this session's pinned memory (from
+  // fdcn_session_host_buffer: a plan written straight into it) is copied to
+  // the device from where it lies; anything else is staged.  The staging
+  // block mirrors the device offsets up to the first array copied directly,
+  // so the common all-staged case is one H2D copy.
+  const bool f_direct = it && s->pinned().owns(payoff, vb);
+  const bool v_host = v_init && !v_is_payoff;
+  const bool v_direct = v_host && s->pinned().owns(v_init, vb);
+  const bool stage_f = it && !f_direct, stage_v = v_host && !v_direct;
+  size_t hsz = pre, hF = 0, hV = 0;
+  if (stage_f) hF = hsz, hsz = oF + al256(vb);
+  if (stage_v) hV = it ? (stage_f ? oV : pre) : oV, hsz = hV + al256(vb);
+  const size_t mirrored = stage_v && hV == oV ? oV + vb : stage_f ? oF + vb : pre;
 
-  char* h = s->pinned().get(staged);
-  if (!h) return sfail(FDCN_ENOMEM, "hipHostMalloc(%zu) failed", staged);
+  char* h = s->pinned().get(hsz);
+  if (!h) return sfail(FDCN_ENOMEM, "hipHostMalloc(%zu) failed", hsz);
   memcpy(h + oP, params, sizeof(double) * B * FDCN_NPARAM);
   memcpy(h + oI, iparams, sizeof(int32_t) * B * FDCN_NIPARAM);
   if (n_mon > 0) {
     memcpy(h + oM, mon_step, sizeof(int32_t) * n_mon);
     memcpy(h + oR, mon_rebate, sizeof(double) * n_mon);
   }
-  if (it) stage_copy(h + oF, payoff, sizeof(double) * nv);
   if (v_init_slots) {
     uint64_t* a = (uint64_t*)(h + oA);
     for (int32_t b = 0; b < B; ++b) a[b] = (uint64_t)s->slots.ptr[v_init_slots[b]];
-  } else if (!v_is_payoff) {
-    stage_copy(h + oV, v_init, sizeof(double) * nv);
   }
+  if (stage_f) stage_copy(h + hF, payoff, vb);
+  if (stage_v) stage_copy(h + hV, v_init, vb);
   hipStream_t st;
   if ((rc = pick_stream(s, &st))) return rc;
   if (v_init_slots && (rc = wait_producers(s, st, B, v_init_slots))) return rc;
   char* d = nullptr;
   if ((rc = alloc_block(s, st, L.size, &d))) return rc;
-  S_TRY(hipMemcpyAsync(d, h, staged, hipMemcpyHostToDevice, st));
+  S_TRY(hipMemcpyAsync(d, h, mirrored, hipMemcpyHostToDevice, st));
+  if (f_direct) S_TRY(hipMemcpyAsync(d + oF, payoff, vb, hipMemcpyHostToDevice, st));
+  if (stage_v && hV != oV) S_TRY(hipMemcpyAsync(d + oV, h + hV, vb, hipMemcpyHostToDevice, st));
+  if (v_direct) S_TRY(hipMemcpyAsync(d + oV, v_init, vb, hipMemcpyHostToDevice, st));
   if (v_init_slots) {
     hipLaunchKernelGGL(gather_rows, dim3(B), dim3(256), 0, st, (const uint64_t*)(d + oA),
                        (double*)(d + oV), n_nodes);

@@ -63,6 +63,14 @@ struct PinnedArenaT {
     used += bytes;
     return r;
   }
+  // [p, p + n) lies inside one chunk this arena holds (a region it handed
+  // out: pinned memory an async copy may read directly)
+  bool owns(const void* p, size_t n) const {
+    const char* c = static_cast<const char*>(p);
+    for (const Chunk& k : chunks)
+      if (c >= k.p && n <= k.cap && c - k.p <= (ptrdiff_t)(k.cap - n)) return true;
+    return false;
+  }
   void reset() { cur = used = 0; }
   void trim(size_t keep) {
     size_t held = 0, k = 0;

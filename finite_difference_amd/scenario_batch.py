@@ -26,6 +26,7 @@ the caller takes the per-row path.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -180,29 +181,35 @@ def _greeks_host(V: np.ndarray, rint: np.ndarray, rdbl: np.ndarray, tpar: np.nda
     return out
 
 
+def _device_session():
+    from .session import Session
+    return Session()
+
+
 def _march_and_finish(eng: Engine, plan: dict, n_time: int, n_ranna: int,
-                      mon: np.ndarray, overlap=None) -> np.ndarray:
+                      mon: np.ndarray, overlap=None, session=None) -> np.ndarray:
     """March the plan's 2R solves as one launch and run the Greeks epilogue.
     ``overlap`` (optional): host work that does not need the march, run
-    while the device marches (the launch is asynchronous)."""
+    while the device marches (the launch is asynchronous).  ``session``: the
+    device session the plan's v_init was built in (device engines)."""
     Q = plan["params"].shape[0]
     g = Group(False, plan["n_nodes"], n_time, min(n_ranna, n_time), plan["params"],
               plan["iparams"], plan["v_init"], None, np.tile(mon, Q), plan["mon_rebate"],
               list(range(Q)))
     RI = plan["rint"]
-    if eng.on_device:
-        from .session import GK_BARRIER, Session
-        with Session() as S:
-            slots = S.march(g)
-            eng.launches += 1
-            eng.solves += Q
-            if overlap is not None:
-                overlap()
-            RI = RI.copy()
-            RI[:, 0] = slots[RI[:, 0]]
-            return S.greeks_raw(np.full(Q // 2, GK_BARRIER, np.int32),
-                                np.arange(0, Q, 2, dtype=np.int32), plan["tparams"], RI,
-                                plan["rdbl"])
+    if session is not None:
+        from .session import GK_BARRIER
+        S = session
+        slots = S.march(g)
+        eng.launches += 1
+        eng.solves += Q
+        if overlap is not None:
+            overlap()
+        RI = RI.copy()
+        RI[:, 0] = slots[RI[:, 0]]
+        return S.greeks_raw(np.full(Q // 2, GK_BARRIER, np.int32),
+                            np.arange(0, Q, 2, dtype=np.int32), plan["tparams"], RI,
+                            plan["rdbl"])
     if overlap is not None:
         overlap()
     V = eng.backend.run_group(g)
@@ -221,6 +228,7 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
     spent in the plan builder ("plan") and in the march + epilogue ("march")."""
     import time
     from . import scenarios
+    t_start = time.perf_counter()
     eng = engine if engine is not None else default_engine()
     bp = dict(base_params)
     R = len(cols["S0"])
@@ -305,22 +313,31 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
         mon = np.asarray(sorted(k for k in p0._monitor_indices_tau(dt) if 1 <= k <= n_time),
                          np.int32)
         t0 = time.perf_counter()
-        try:
-            plan = capi.barrier_plan(
-                row, flag, T, int(p0._requested_space_nodes), n_time,
-                1 if p0.grid_mode == "explicit" else 0, tail_quantile(), dv_sigma,
-                bool(p0.rebate_at_hit), mon)
-        except capi.FdcnError as e:
-            if "differ" in str(e):
-                return None  # two launch shapes: the per-row path groups them
-            raise
-        t1 = time.perf_counter()
-        # the Black-76 legs run on the host while the device marches
-        res = _march_and_finish(eng, plan, n_time, int(p0.rannacher_steps), mon,
-                                overlap=black76_legs)
+        with (_device_session() if eng.on_device else contextlib.nullcontext()) as S:
+            try:
+                # on the device the initial vectors are written straight into
+                # the session's pinned memory (no staging copy, no page
+                # faults or unmapping of a fresh 100+ MB array per file)
+                plan = capi.barrier_plan(
+                    row, flag, T, int(p0._requested_space_nodes), n_time,
+                    1 if p0.grid_mode == "explicit" else 0, tail_quantile(), dv_sigma,
+                    bool(p0.rebate_at_hit), mon,
+                    v_init_out=None if S is None else S.host_buffer)
+            except capi.FdcnError as e:
+                if "differ" in str(e):
+                    return None  # two launch shapes: the per-row path groups them
+                raise
+            t1 = time.perf_counter()
+            # the Black-76 legs run on the host while the device marches
+            res = _march_and_finish(eng, plan, n_time, int(p0.rannacher_steps), mon,
+                                    overlap=black76_legs, session=S)
+            del plan  # the pinned view goes before the session closes
+            t2 = time.perf_counter()
         if timing is not None:
+            timing["prep"] = t0 - t_start
             timing["plan"] = t1 - t0
-            timing["march"] = time.perf_counter() - t1
+            timing["march"] = t2 - t1
+            timing["free"] = time.perf_counter() - t2
         for j, k in enumerate(GREEKS):
             out[k][pde] = res[:, j]
     # knocked-out rows (already_hit, :907-946): the rebate discounted from the

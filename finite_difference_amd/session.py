@@ -42,6 +42,8 @@ def _bind(L: ctypes.CDLL) -> None:
     L.fdcn_session_destroy.argtypes = [_V]
     L.fdcn_session_slots.restype = _I
     L.fdcn_session_slots.argtypes = [_V]
+    L.fdcn_session_host_buffer.restype = _I
+    L.fdcn_session_host_buffer.argtypes = [_V, ctypes.c_int64, ctypes.POINTER(_V)]
     L.fdcn_session_march.restype = _I
     L.fdcn_session_march.argtypes = [_V, _I, _I, _I, _I, _I, _V, _V, _V, _V, _V, _I, _V, _V, _V]
     L.fdcn_session_dividend_jump.restype = _I
@@ -137,6 +139,16 @@ class Session:
             self.close()
         except Exception:
             pass
+
+    def host_buffer(self, n: int) -> np.ndarray:
+        """n float64 of the session's pinned host memory (fdcn_session_host_buffer).
+        A march whose payoff / v_init lies in it copies it to the device
+        without staging, asynchronously: leave it unchanged until the next
+        greeks_raw / fetch, and drop the array before the session closes
+        (the memory is the session's, recycled after close)."""
+        p = _V()
+        capi._check(self._L.fdcn_session_host_buffer(self._h, 8 * max(int(n), 1), ctypes.byref(p)))
+        return np.ctypeslib.as_array(ctypes.cast(p, _PD), shape=(max(int(n), 1),))[:int(n)]
 
     # -- steps ---------------------------------------------------------------
     def march(self, g, v_init_slots: Optional[np.ndarray] = None) -> np.ndarray:

@@ -175,11 +175,23 @@ int fdcn_session_create(fdcn_session** out);
 int fdcn_session_destroy(fdcn_session* s);
 int fdcn_session_slots(const fdcn_session* s);  /* slots created so far */
 
+/* `bytes` of pinned host memory owned by the session, valid until
+ * fdcn_session_destroy (256-byte aligned).  A caller that builds a march's
+ * payoff / v_init directly in it (the whole-file plans: 100-400 MB) spares
+ * the staging copy: fdcn_session_march copies such an array to the device
+ * from where it lies, asynchronously, so its contents must stay unchanged
+ * until the session's next synchronising call (fdcn_session_greeks /
+ * fdcn_session_fetch) or its destruction. */
+int fdcn_session_host_buffer(fdcn_session* s, int64_t bytes, void** out);
+
 /* One batched march (the fdcn_cn_batch / fdcn_it_batch plan; it != 0 for
  * Ikonen-Toivanen).  Initial vectors come from the host (v_init [B][n_nodes])
  * or from earlier slots (v_init_slots [B]); pass exactly one.  An IT march
- * may pass its payoff pointer as v_init (the array is staged once).  The B
- * outputs become new slots, numbers written to out_slots [B]. */
+ * may pass its payoff pointer as v_init (the array is copied once).  Host
+ * arrays are staged through pinned memory before the call returns, except a
+ * payoff / v_init inside an fdcn_session_host_buffer region (read later, by
+ * the asynchronous copy).  The B outputs become new slots, numbers written
+ * to out_slots [B]. */
 int fdcn_session_march(fdcn_session* s, int32_t it, int32_t B, int32_t n_nodes, int32_t n_time,
                        int32_t n_ranna, const double* params, const int32_t* iparams,
                        const double* v_init, const int32_t* v_init_slots, const double* payoff,

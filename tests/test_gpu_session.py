@@ -318,3 +318,38 @@ def test_destroy_drains_cross_stream_consumers_before_freeing():
     want = o.run(cons)
     for g, w in zip(got, want):
         assert np.max(np.abs(g - w)) <= 1e-10 * max(1.0, np.max(np.abs(w)))
+
+
+@pytest.mark.parametrize("where", ["v_direct", "payoff_is_v_direct", "payoff_direct_v_staged",
+                                   "both_direct"])
+def test_host_buffer_inputs_march_bitwise_as_staged(where):
+    """fdcn_session_host_buffer: a payoff / v_init written into the session's
+    pinned memory is copied to the device from there (no staging), in every
+    combination the march's upload handles -- the CN march with v_init direct,
+    the IT march with its payoff direct and v_init staged, v_init == payoff
+    direct, both direct -- and the outputs equal the all-staged march bit for bit."""
+    rng = np.random.default_rng(77)
+    it = where != "v_direct"
+    solves = [random_solve(rng, 1025, 48, 2, it=it) for _ in range(6)]
+    g = pack(solves, list(range(len(solves))))
+    if where == "payoff_is_v_direct":
+        g.v_init = g.payoff  # the first segment of an American grid
+    with Session() as S:
+        ref = S.fetch(S.march(g), g.n_nodes)
+
+        def pinned(a):
+            buf = S.host_buffer(a.size).reshape(a.shape)
+            buf[...] = a
+            return buf
+        import dataclasses
+        h = dataclasses.replace(g)
+        if where in ("v_direct", "both_direct"):
+            h.v_init = pinned(g.v_init)
+        if where in ("payoff_direct_v_staged", "both_direct"):
+            h.payoff = pinned(g.payoff)
+        if where == "payoff_is_v_direct":
+            h.payoff = pinned(g.payoff)
+            h.v_init = h.payoff
+        got = S.fetch(S.march(h), g.n_nodes)
+        del h
+    assert np.array_equal(got, ref)

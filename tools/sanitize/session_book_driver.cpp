@@ -62,9 +62,22 @@ void session_round(fdcn_book::PinnedArenaT<MallocAlloc>& arena, unsigned seed, s
     for (auto& r : live)                // and disjoint from the live regions
       CHECK(p + (n ? n : 1) <= r.first || r.first + (r.second ? r.second : 1) <= p);
     live.push_back({p, n});
+    CHECK(arena.owns(p, n ? n : 1));  // a handed-out region is pinned memory
   }
   for (size_t i = 0; i < live.size(); ++i)  // nothing was overwritten since
     if (live[i].second) CHECK((unsigned char)live[i].first[live[i].second - 1] == (i & 0xff));
+}
+
+void test_owns() {
+  fdcn_book::PinnedArenaT<MallocAlloc> arena;
+  char* p = arena.get(1000);
+  const size_t cap = arena.chunks[0].cap;
+  CHECK(arena.owns(p, 1000) && arena.owns(p + 17, 983) && arena.owns(p, cap));
+  CHECK(!arena.owns(p, cap + 1) && !arena.owns(p + cap, 1) && !arena.owns(p - 1, 8));
+  std::vector<double> heap(64);  // caller memory that is not the arena's
+  CHECK(!arena.owns(heap.data(), sizeof(double) * heap.size()));
+  arena.reset();
+  arena.trim(0);
 }
 
 void test_arena() {
@@ -112,6 +125,7 @@ void test_slots() {
 
 int main() {
   test_layout();
+  test_owns();
   test_arena();
   test_slots();
   printf("session_book_driver: ok\n");
