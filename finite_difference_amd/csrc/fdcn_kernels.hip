@@ -715,6 +715,16 @@ fdcn_march(KArgs A) {
   double mulLF = 0.0, mulLB = 0.0;  // products across the last sub-chain
   double fmM = 0.0, bmM = 0.0;      // products across a full sub-chain
   int nst_f = 6, nst_b = 6;         // scan stages that carry weight above 1e-18
+  // kRec: the phase's |fm|^(NPT/2) and |bm|^(NPT/2) are below 1e-18, so the
+  // zero-carry aggregates need only half a chunk (solve_rec_half)
+  bool rec_half = false;
+  // kRec (solve_rec), per phase: the product of the forward multipliers
+  // over the chunk's last quarter (fm^(Q-1) mlast, per lane: short lanes
+  // end one node early); uniform fm^(H-1) and bm^H for the rare branch
+  double recQ = 0.0, rec_fmH1 = 0.0, rec_bmH = 0.0;
+  (void)recQ;
+  (void)rec_fmH1;
+  (void)rec_bmH;
   Phase ph;
   // Step forms (see the time loop):
   //   IT            state (V, Q), pointwise rhs V + Q, solve in place on V
@@ -853,6 +863,13 @@ fdcn_march(KArgs A) {
       while (nb < kMaxSt && qb > 1e-18) { qb *= qb; ++nb; }
       nst_f = kPair ? umax_halves(nf) : uni_i(nf);
       nst_b = kPair ? umax_halves(nb) : uni_i(nb);
+      if constexpr (rec_form(IT, W, NPT)) {
+        const double hf = fabs(pow_n<NPT>(p.fm, NPT / 2)), hb = fabs(pow_n<NPT>(p.bm, NPT / 2));
+        rec_half = uni_i(hf < 1e-18 && hb < 1e-18) != 0;
+        rec_fmH1 = U(pow_n<NPT>(p.fm, NPT / 2 - 1));
+        rec_bmH = U(pow_n<NPT>(p.bm, NPT / 2));
+        recQ = pow_n<NPT>(p.fm, NPT / 4 - 1) * mlast;
+      }
     }
     if constexpr (W > 1) {
       if (lane == 63) xch[Xch<W>::kFtot + wave] = Fpre;
@@ -1110,6 +1127,118 @@ fdcn_march(KArgs A) {
         }
       }
     }
+  };
+
+  // The recovery form's solve (kRec; replaces solve() there).  A chunk's
+  // zero-carry aggregate -- what the right neighbour's carry is made of --
+  // sums its nodes with weights fm^(distance to the chunk's end).  When the
+  // phase's |fm|^(NPT/2) and |bm|^(NPT/2) are below 1e-18 (rec_half: config
+  // 5's Crank-Nicolson phase, |fm| ~ 0.2 at NPT = 64) the first half's
+  // weights fall under the 1e-18 cut the scan stages and the
+  // Sherman-Morrison extent use (and the scan stages carry nothing either):
+  // the forward aggregate takes the second half, the backward one the first
+  // half.  Otherwise (the Rannacher steps) a uniform branch adds the other
+  // halves and the scan stages; it only reads V.
+  // Forward pass 1 runs the aggregate's two quarters as two chains joined
+  // by one FMA; pass 2 runs the first half as one chain, then the second
+  // half with the backward aggregate of the first half (which reads only
+  // final values) alongside; backward pass 2 is fused with the update.
+  // Plain FMAs where the compiler can schedule them: around inline asm it
+  // pads dependent v_fma_f64 pairs with s_nop (an issue slot each), which a
+  // lone asm chain paid on every link.  A lone chain of plain FMAs costs ~6
+  // cycles per link against ~4.2 for independent ones (one wave,
+  // tools/ubench/fma64_latency.hip), so a chain is split only where the
+  // split is cheap.  Per node-step 4 + ~1 FMAs against 6 + the joins.
+  auto solve_rec = [&](const Phase& p) __attribute__((always_inline)) {
+    constexpr int H = NPT / 2, Q = NPT / 4;
+    const double fm = p.fm, bm = p.bm;
+    FDCN_PRIO_HI();
+    double a2 = V[H], a3 = V[H + Q];
+#pragma unroll
+    for (int i = 1; i < Q; ++i) {
+      a2 = fma(fm, a2, V[H + i]);
+      a3 = fma(H + Q + i == NPT - 1 ? mlast : fm, a3, V[H + Q + i]);
+    }
+    double w = fma(recQ, a2, a3);  // the second half's aggregate
+    if (!rec_half) {
+      // the first half enters with the second half's multipliers
+      double a0 = V[0];
+#pragma unroll
+      for (int i = 1; i < H; ++i) a0 = fma(fm, a0, V[i]);
+      w = fma(rec_fmH1 * mlast, a0, w);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const double wf = (kScanLds && j >= 2) ? sw[(j - 2) * 128 + lane] : FW[j];
+        if (j < nst_f) w = fma(wf, scan_up(w, 1 << j, lane4), w);
+      }
+    }
+    const double cin = shfl_up1(w, 1);  // lane 0 receives 0
+    FDCN_PRIO_LO();
+    // forward pass 2 over the first half from the carry (fm_act: 0 on
+    // inactive lanes)
+    V[0] = fma(fm_act, cin, V[0]);
+#pragma unroll
+    for (int k = 1; k < H; ++k) V[k] = fma(fm, V[k - 1], V[k]);
+    // the second half, with the backward zero-carry aggregate of nodes
+    // H-1..0 alongside
+    double y = V[H - 1];
+#pragma unroll
+    for (int k = H; k < NPT; ++k) {
+      V[k] = fma(k == NPT - 1 ? mlast2 : fm, V[k - 1], V[k]);
+      const int kb = H - 1 - (k - H + 1);
+      if (kb >= 0) y = fma(bm, y, V[kb]);
+    }
+    FDCN_PRIO_HI();
+    if (!rec_half) {
+      // nodes NPT-1..H enter the backward aggregate with bm^H
+      double y2 = V[NPT - 1];
+#pragma unroll
+      for (int k = NPT - 2; k >= H; --k) y2 = fma(bm, y2, V[k]);
+      y = fma(rec_bmH, y2, y);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const double wg = (kScanLds && j >= 2) ? sw[(j - 2) * 128 + 64 + lane] : GW[j];
+        if (j < nst_b) y = fma(wg, scan_dn(y, 1 << j, lane4), y);
+      }
+    }
+    const double cinb = shfl_dn1(y, 1);  // lane 63 receives 0
+    FDCN_PRIO_LO();
+    // backward pass 2 fused with the update, per node (descending), as in
+    // solve(): u = bm u + w_k; -V_k = fm w_{k-1} - w_k (+ boundary term);
+    // x_k = s u - V_k over V[k].  Software-pipelined so no FMA reads a
+    // result of the two instructions before it (that costs an s_nop):
+    // group k issues the chain step of node k, the recovery of node k-1 and
+    // the update of node k+1 (whose forward value every reader has used)
+    double uc = cinb;
+    double tt[NPT], ucs[NPT];
+    auto rec_tt = [&](int k) __attribute__((always_inline)) {
+      const double wprev = (k == 0) ? cin : V[k - 1];
+      const double mk = (k == NPT - 1) ? mlast2 : (k == 0 ? fm_act : fm);
+      tt[k] = fma(mk, wprev, -V[k]);
+      if (k == NPT - 1) tt[k] = fma(e_last, rec_hi, tt[k]);
+      if (k == 0) tt[k] = fma(e_first, rec_lo, tt[k]);
+    };
+    auto rec_upd = [&](int k) __attribute__((always_inline)) {
+      // in V[k]'s register (asm: the compiler's accumulate form would
+      // first copy tt there)
+      if (k == NPT - 1)
+        asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "v"(s_l), "v"(ucs[k]), "v"(tt[k]));
+      else
+        asm volatile("v_fma_f64 %0, %1, %2, %3" : "+v"(V[k]) : "s"(p.s), "v"(ucs[k]), "v"(tt[k]));
+    };
+    rec_tt(NPT - 1);
+#pragma unroll
+    for (int k = NPT - 1; k >= 0; --k) {
+      if (k == NPT - 1)
+        asm volatile("v_fma_f64 %0, %1, %2, %3" : "=v"(ucs[k]) : "v"(glast), "v"(uc), "v"(V[k]));
+      else
+        asm volatile("v_fma_f64 %0, %1, %2, %3" : "=v"(ucs[k]) : "s"(bm), "v"(uc), "v"(V[k]));
+      uc = ucs[k];
+      if (k >= 1) rec_tt(k - 1);
+      if (k + 1 < NPT) rec_upd(k + 1);
+    }
+    rec_upd(0);
+    y0c = uc;
   };
 
   // Two-pass solve (kTP, W = 1): both zero-carry passes in place on Wr, the
@@ -1820,7 +1949,7 @@ fdcn_march(KArgs A) {
       // one fused solve for both phases (a second, plain solve for the
       // Rannacher steps doubled the live ranges: 373 registers, one wave per
       // SIMD, 47.8 ms per config-5 launch instead of 26)
-      solve(ph, std::true_type{});
+      solve_rec(ph);
       static_assert(!kRec || NPT % 8 == 0, "recovery variants add back 8 slots per group");
       if (m < A.n_ranna) {
         // x = (s u - V_old) + V_old, eight slots per group so the loads do
