@@ -327,6 +327,10 @@ typedef unsigned KoMask16 __attribute__((ext_vector_type(16)));  // 8 masks, s_l
 __device__ __forceinline__ unsigned long long ko_pair(KoMask16 m, int j) {
   return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];
 }
+typedef unsigned KoMask8 __attribute__((ext_vector_type(8)));  // 4 masks, s_load_dwordx8
+__device__ __forceinline__ unsigned long long ko_pair8(KoMask8 m, int j) {
+  return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];
+}
 // Only the one-wave throughput variants reload from NPT = 16 on: the latency
 // variants (several waves, or the single-trade flavour) have a knock-out on
 // the critical path of one trade, where the s_load latency of every monitor
@@ -2122,37 +2126,36 @@ fdcn_march(KArgs A) {
         // addresses out of the time loop and spill them)
         unsigned long long ka = kPair ? (hit1 ? (hit2 ? kom_addr12 : kom_addr) : kom_addr2) : kom_addr;
         asm volatile("" : "+s"(ka));
-        KoMask16 mcur;
-        asm volatile("s_load_dwordx16 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)"
+        // four slots per block, double-buffered (s_load_dwordx8: 16 SGPRs
+        // for both buffers; eight-slot blocks held 32 and pushed other
+        // uniform values out to VGPR lanes, read back every step)
+        KoMask8 mcur;
+        asm volatile("s_load_dwordx8 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)"
                      : "=s"(mcur)
                      : "s"(ka)
                      : "memory");
 #pragma unroll
-        for (int g = 0; g < NPT / 8; ++g) {
-          KoMask16 mnxt;
-          const bool more = g + 1 < NPT / 8;
+        for (int g = 0; g < NPT / 4; ++g) {
+          KoMask8 mnxt;
+          const bool more = g + 1 < NPT / 4;
           unsigned long long sv;
 #define FDCN_KO_MOV(j) "s_and_b64 exec, %[m" #j "], %[sv]\n\tv_mov_b64 %[v" #j "], %[rb]\n\t"
 #define FDCN_KO_OPS                                                                  \
-  [v0] "+v"(V[8 * g]), [v1] "+v"(V[8 * g + 1]), [v2] "+v"(V[8 * g + 2]),             \
-      [v3] "+v"(V[8 * g + 3]), [v4] "+v"(V[8 * g + 4]), [v5] "+v"(V[8 * g + 5]),     \
-      [v6] "+v"(V[8 * g + 6]), [v7] "+v"(V[8 * g + 7]), [sv] "=&s"(sv)
+  [v0] "+v"(V[4 * g]), [v1] "+v"(V[4 * g + 1]), [v2] "+v"(V[4 * g + 2]),             \
+      [v3] "+v"(V[4 * g + 3]), [sv] "=&s"(sv)
 #define FDCN_KO_INS                                                                     \
-  [rb] "v"(rebv), [m0] "s"(ko_pair(mcur, 0)), [m1] "s"(ko_pair(mcur, 1)),                \
-      [m2] "s"(ko_pair(mcur, 2)), [m3] "s"(ko_pair(mcur, 3)), [m4] "s"(ko_pair(mcur, 4)), \
-      [m5] "s"(ko_pair(mcur, 5)), [m6] "s"(ko_pair(mcur, 6)), [m7] "s"(ko_pair(mcur, 7))
+  [rb] "v"(rebv), [m0] "s"(ko_pair8(mcur, 0)), [m1] "s"(ko_pair8(mcur, 1)),              \
+      [m2] "s"(ko_pair8(mcur, 2)), [m3] "s"(ko_pair8(mcur, 3))
           if (more) {
-            asm volatile("s_mov_b64 %[sv], exec\n\ts_load_dwordx16 %[mn], %[ga], 0\n\t"
+            asm volatile("s_mov_b64 %[sv], exec\n\ts_load_dwordx8 %[mn], %[ga], 0\n\t"
                          FDCN_KO_MOV(0) FDCN_KO_MOV(1) FDCN_KO_MOV(2) FDCN_KO_MOV(3)
-                         FDCN_KO_MOV(4) FDCN_KO_MOV(5) FDCN_KO_MOV(6) FDCN_KO_MOV(7)
                          "s_mov_b64 exec, %[sv]\n\ts_waitcnt lgkmcnt(0)"
                          : FDCN_KO_OPS, [mn] "=&s"(mnxt)
-                         : FDCN_KO_INS, [ga] "s"(ka + 64ull * (g + 1))
+                         : FDCN_KO_INS, [ga] "s"(ka + 32ull * (g + 1))
                          : "memory", "scc");
           } else {
             asm volatile("s_mov_b64 %[sv], exec\n\t"
                          FDCN_KO_MOV(0) FDCN_KO_MOV(1) FDCN_KO_MOV(2) FDCN_KO_MOV(3)
-                         FDCN_KO_MOV(4) FDCN_KO_MOV(5) FDCN_KO_MOV(6) FDCN_KO_MOV(7)
                          "s_mov_b64 exec, %[sv]"
                          : FDCN_KO_OPS
                          : FDCN_KO_INS
