@@ -242,3 +242,42 @@ def test_split_two_pass_every_step_knockout_vs_oracle(ko_lo, force_variant):
         solves.append(s)
     assert capi.variant_name(n_nodes, False, B=6) == "fdcn_march<0,1,16,0>"
     _compare(solves, f"split two-pass every-step KO ko_lo={ko_lo}")
+
+
+def _fm(a, c, bc, dt, theta):
+    """The converged forward multiplier fm = -A_L / r of A = I - theta dt L
+    (r: the larger root of r^2 - A_C r + A_L A_U = 0), as the kernel's phase."""
+    AL, AC, AU = -theta * dt * a, 1.0 - theta * dt * bc, -theta * dt * c
+    r = 0.5 * (AC + np.sqrt(AC * AC - 4.0 * AL * AU))
+    return -AL / r
+
+
+@pytest.mark.parametrize("n_nodes", [4096, 4097, 3000], ids=["short2", "full", "npt48"])
+def test_rec_form_half_chunk_aggregates_vs_oracle(n_nodes, force_variant):
+    """The recovery form's half-chunk aggregates (solve_rec, rec_half): grids
+    with dt sigma^2 / dx^2 ~ 1 (config 5's regime), so the Crank-Nicolson
+    phase's |fm|^(NPT/2) is below 1e-18 (aggregates over half a chunk, no
+    scan stages) while the two Rannacher steps' is not (the uniform branch
+    that adds the other halves): both paths in one march, with a knock-out
+    on every step, short lanes (4096 nodes: two), a full layout (4097) and
+    the 48-node chunks (3000 nodes)."""
+    npt = 48 if n_nodes == 3000 else 64
+    force_variant(1, npt)
+    rng = np.random.default_rng(77 + n_nodes)
+    solves = []
+    for i in range(6):
+        s = random_solve(rng, n_nodes, 80, 2, it=False, ko=False)
+        a, c, bc = s.coeffs
+        # dt a in a band where the CN phase's |fm|^(NPT/2) is < 1e-18 and the
+        # Rannacher phase's is not
+        s.dt = ((0.6 + 0.04 * i) if npt == 64 else (0.3 + 0.03 * i)) / a
+        fm_cn, fm_r = _fm(a, c, bc, s.dt, 0.5), _fm(a, c, bc, s.dt, 1.0)
+        bm_cn = _fm(c, a, bc, s.dt, 0.5)
+        assert abs(fm_cn) ** (npt // 2) < 1e-18 and abs(bm_cn) ** (npt // 2) < 1e-18, (fm_cn, bm_cn)
+        assert abs(fm_r) ** (npt // 2) > 1e-18, fm_r  # the Rannacher steps take the branch
+        s.ko_lo, s.ko_hi = int(rng.integers(-1, 600)), int(rng.integers(n_nodes - 700, n_nodes + 2))
+        s.mon_steps = list(range(1, s.n_time + 1))
+        s.mon_rebates = [0.0 if i % 2 else 0.4] * s.n_time
+        solves.append(s)
+    assert capi.plan(n_nodes, False, B=6)["npt"] == npt
+    _compare(solves, f"rec half-chunk aggregates n={n_nodes}")
