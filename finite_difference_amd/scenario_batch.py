@@ -26,7 +26,6 @@ the caller takes the per-row path.
 """
 from __future__ import annotations
 
-import contextlib
 from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -187,35 +186,85 @@ def _device_session():
 
 
 def _march_and_finish(eng: Engine, plan: dict, n_time: int, n_ranna: int,
-                      mon: np.ndarray, overlap=None, session=None) -> np.ndarray:
-    """March the plan's 2R solves as one launch and run the Greeks epilogue.
-    ``overlap`` (optional): host work that does not need the march, run
-    while the device marches (the launch is asynchronous).  ``session``: the
-    device session the plan's v_init was built in (device engines)."""
+                      mon: np.ndarray, overlap=None) -> np.ndarray:
+    """A host engine's march of the plan's 2R solves (one run_group) and the
+    Greeks epilogue on the host (the CPU-oracle test path; device engines
+    take _plan_march_device).  ``overlap`` (optional): host work run first."""
     Q = plan["params"].shape[0]
     g = Group(False, plan["n_nodes"], n_time, min(n_ranna, n_time), plan["params"],
               plan["iparams"], plan["v_init"], None, np.tile(mon, Q), plan["mon_rebate"],
               list(range(Q)))
     RI = plan["rint"]
-    if session is not None:
-        from .session import GK_BARRIER
-        S = session
-        slots = S.march(g)
-        eng.launches += 1
-        eng.solves += Q
-        if overlap is not None:
-            overlap()
-        RI = RI.copy()
-        RI[:, 0] = slots[RI[:, 0]]
-        return S.greeks_raw(np.full(Q // 2, GK_BARRIER, np.int32),
-                            np.arange(0, Q, 2, dtype=np.int32), plan["tparams"], RI,
-                            plan["rdbl"])
     if overlap is not None:
         overlap()
     V = eng.backend.run_group(g)
     eng.launches += 1
     eng.solves += Q
     return _greeks_host(V, RI, plan["rdbl"], plan["tparams"])
+
+
+# the device path plans and marches the rows in chunks: the plan of chunk
+# i+1 is built on the host while chunk i's initial vectors cross PCIe and it
+# marches.  Two chunks from 4096 PDE rows on: a 10 000-row file 16.4 -> 13.0
+# ms, three 13.2, four 14.9, eight 14.8 (tools/chunk_sweep.py; more chunks
+# slow the plan builder, whose writes then share host memory with the DMA)
+CHUNK_ROWS = 2048
+MAX_CHUNKS = 2
+
+
+def _plan_march_device(eng: Engine, S, row: np.ndarray, flag: np.ndarray, plan_args: tuple,
+                       n_time: int, n_ranna: int, mon: np.ndarray, overlap,
+                       timing: Optional[Dict[str, float]]) -> Optional[np.ndarray]:
+    """The device path of price_columns, pipelined: the rows in up to
+    MAX_CHUNKS chunks of at least CHUNK_ROWS, each planned straight into the session's pinned memory
+    and marched as one asynchronous launch (H2D + kernel) while the host
+    plans the next; one Greeks epilogue over all rows at the end.  The
+    solves are the same as one launch's (each scenario is its own
+    wavefront), so the results are too.  None when the chunks' grids differ
+    (the per-row path groups them)."""
+    import time
+    from .session import GK_BARRIER
+    Rp = row.shape[0]
+    n_chunks = max(1, min(MAX_CHUNKS, Rp // CHUNK_ROWS))
+    bounds = [Rp * i // n_chunks for i in range(n_chunks + 1)]
+    t_plan = 0.0
+    n_nodes = None
+    RIs, rdbls, tps = [], [], []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        t0 = time.perf_counter()
+        try:
+            plan = capi.barrier_plan(row[a:b], flag[a:b], *plan_args, v_init_out=S.host_buffer)
+        except capi.FdcnError as e:
+            if "differ" in str(e):
+                return None  # two launch shapes: the per-row path groups them
+            raise
+        t_plan += time.perf_counter() - t0
+        if n_nodes is None:
+            n_nodes = plan["n_nodes"]
+        elif plan["n_nodes"] != n_nodes:
+            return None
+        Q = plan["params"].shape[0]
+        g = Group(False, plan["n_nodes"], n_time, min(n_ranna, n_time), plan["params"],
+                  plan["iparams"], plan["v_init"], None, np.tile(mon, Q), plan["mon_rebate"],
+                  list(range(Q)))
+        slots = S.march(g)
+        eng.launches += 1
+        eng.solves += Q
+        RI = plan["rint"].copy()
+        RI[:, 0] = slots[RI[:, 0]]
+        RIs.append(RI)
+        rdbls.append(plan["rdbl"])
+        tps.append(plan["tparams"])
+        del plan, g  # the pinned view (the session keeps the memory until it closes)
+    t1 = time.perf_counter()
+    if overlap is not None:
+        overlap()
+    res = S.greeks_raw(np.full(Rp, GK_BARRIER, np.int32), np.arange(0, 2 * Rp, 2, dtype=np.int32),
+                       np.concatenate(tps), np.concatenate(RIs), np.concatenate(rdbls))
+    if timing is not None:
+        timing["plan"] = t_plan
+        timing["march"] = time.perf_counter() - t1
+    return res
 
 
 def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
@@ -312,32 +361,35 @@ def price_columns(cols: Dict[str, Sequence], base_params: Dict[str, Any],
         dt = T / n_time
         mon = np.asarray(sorted(k for k in p0._monitor_indices_tau(dt) if 1 <= k <= n_time),
                          np.int32)
+        plan_args = (T, int(p0._requested_space_nodes), n_time,
+                     1 if p0.grid_mode == "explicit" else 0, tail_quantile(), dv_sigma,
+                     bool(p0.rebate_at_hit), mon)
+        n_ranna = int(p0.rannacher_steps)
         t0 = time.perf_counter()
-        with (_device_session() if eng.on_device else contextlib.nullcontext()) as S:
+        if eng.on_device:
+            # the Black-76 legs run on the host while the device marches
+            with _device_session() as S:
+                res = _plan_march_device(eng, S, row, flag, plan_args, n_time, n_ranna, mon,
+                                         black76_legs, timing)
+                t2 = time.perf_counter()
+            if res is None:
+                return None
+            if timing is not None:
+                timing["prep"] = t0 - t_start
+                timing["free"] = time.perf_counter() - t2
+        else:
             try:
-                # on the device the initial vectors are written straight into
-                # the session's pinned memory (no staging copy, no page
-                # faults or unmapping of a fresh 100+ MB array per file)
-                plan = capi.barrier_plan(
-                    row, flag, T, int(p0._requested_space_nodes), n_time,
-                    1 if p0.grid_mode == "explicit" else 0, tail_quantile(), dv_sigma,
-                    bool(p0.rebate_at_hit), mon,
-                    v_init_out=None if S is None else S.host_buffer)
+                plan = capi.barrier_plan(row, flag, *plan_args)
             except capi.FdcnError as e:
                 if "differ" in str(e):
                     return None  # two launch shapes: the per-row path groups them
                 raise
             t1 = time.perf_counter()
-            # the Black-76 legs run on the host while the device marches
-            res = _march_and_finish(eng, plan, n_time, int(p0.rannacher_steps), mon,
-                                    overlap=black76_legs, session=S)
-            del plan  # the pinned view goes before the session closes
-            t2 = time.perf_counter()
-        if timing is not None:
-            timing["prep"] = t0 - t_start
-            timing["plan"] = t1 - t0
-            timing["march"] = t2 - t1
-            timing["free"] = time.perf_counter() - t2
+            res = _march_and_finish(eng, plan, n_time, n_ranna, mon, overlap=black76_legs)
+            if timing is not None:
+                timing["prep"] = t0 - t_start
+                timing["plan"] = t1 - t0
+                timing["march"] = time.perf_counter() - t1
         for j, k in enumerate(GREEKS):
             out[k][pde] = res[:, j]
     # knocked-out rows (already_hit, :907-946): the rebate discounted from the

@@ -200,13 +200,16 @@ def test_prefetch_many_device_matches_single_trades():
 
 
 @pytest.mark.parametrize("opt", ["put", "call"])
-def test_vectorized_scenario_file_equals_batched_runner(opt):
-    """scenario_batch (native plan, one launch, device epilogue) against
-    run_rows_batched on the same GPU: the same 2R solves in the same order,
-    so bitwise; and the host epilogue over the same vectors, bitwise."""
+@pytest.mark.parametrize("chunk_rows", [2048, 3], ids=["one_chunk", "two_chunks"])
+def test_vectorized_scenario_file_equals_batched_runner(opt, chunk_rows, monkeypatch):
+    """scenario_batch (native plan, device epilogue; with two_chunks the
+    rows planned and marched in two pipelined chunks) against
+    run_rows_batched on the same GPU: the same 2R solves, so bitwise; and the
+    host epilogue over the same vectors, bitwise."""
     import math
     import test_scenario_batch as T
     from finite_difference_amd import scenario_batch
+    monkeypatch.setattr(scenario_batch, "CHUNK_ROWS", chunk_rows)
     base = scenarios.runner_base_params(opt, 64)
     base.update(num_time_steps=40, grid_mode="explicit", rebate_amount=0.5)
     rows = T._rows(40, 9)
