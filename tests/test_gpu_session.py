@@ -247,13 +247,16 @@ def test_run_all_scenarios_file_on_device(tmp_path):
 
 @pytest.mark.parametrize("divs", [None, [(__import__("datetime").date(2025, 8, 11), 1.5)]],
                          ids=["nodiv", "div1"])
-def test_vectorized_american_file_equals_per_row_device(divs):
+@pytest.mark.parametrize("chunk_rows", [500, 5], ids=["one_chunk", "two_chunks"])
+def test_vectorized_american_file_equals_per_row_device(divs, chunk_rows, monkeypatch):
     """american_batch (native plan, lock-step segment launches, device jumps
-    and epilogue) against the per-row façades' device path (greeks_many) on
-    the same GPU: the same grids in launches of the same shapes, so bitwise."""
+    and epilogue; with two_chunks the rows planned and launched in two
+    pipelined chunks) against the per-row façades' device path (greeks_many)
+    on the same GPU: the same grids, so bitwise."""
     import test_american_batch as T
     from finite_difference_amd import american_batch
     from finite_difference_amd.american import prefetch_many
+    monkeypatch.setattr(american_batch, "CHUNK_ROWS", chunk_rows)
     for opt in ("put", "call"):
         base = T._base(opt, divs, n=128, m=96)
         rows = T._rows(12, 4)
