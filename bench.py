@@ -736,7 +736,9 @@ def bench_scenario_file(args):
         "data": "synthetic scenario file (config_scenarios.csv trade swept over K, sigma, "
                 "barriers; two curves)",
         "config": {"workload": f"scenario_file_{R}rows_{N}x{M}", "config": "BASELINE configs[2]",
-                   "rows": R, "pde_rows": n_pde, "solves": 2 * n_pde},
+                   "rows": R, "pde_rows": n_pde, "solves": 2 * n_pde,
+                   "plan_chunks": max(1, min(scenario_batch.MAX_CHUNKS,
+                                             n_pde // scenario_batch.CHUNK_ROWS))},
         "host_ms": ms - march_ms, "plan_ms": avg["plan"], "march_and_epilogue_ms": march_ms,
         "host_parts_ms": {k: avg[k] for k in ("prep", "plan", "free") if k in avg},
         "outputs_finite": bool(np.all(np.isfinite(out["model_price"])))}), flush=True)
@@ -789,7 +791,9 @@ def bench_american_file(args):
         "data": "synthetic American put file (notebook trade swept over spot, strike, vol; "
                 "two curves)",
         "config": {"workload": f"american_file_{R}rows_{N}x{M}", "config": "BASELINE configs[1]",
-                   "rows": R, "grids_per_row": 6},
+                   "rows": R, "grids_per_row": 6,
+                   "plan_chunks": max(1, min(american_batch.MAX_CHUNKS,
+                                             R // american_batch.CHUNK_ROWS))},
         "host_ms": ms - march_ms, "plan_ms": avg["plan"], "march_and_epilogue_ms": march_ms,
         "host_parts_ms": {k: avg[k] for k in ("prep", "plan", "free") if k in avg},
         "node_steps_per_s": node_steps / (ms * 1e-3),
