@@ -323,10 +323,6 @@ struct MonRun {
 // exec-masked v_mov_b64 per slot.  (NPT = 16 joined in round 2: config 3,
 // daily monitoring, 4 VALU per wave and step fewer on average.)
 constexpr int kKoRow = 32;
-typedef unsigned KoMask16 __attribute__((ext_vector_type(16)));  // 8 masks, s_load_dwordx16
-__device__ __forceinline__ unsigned long long ko_pair(KoMask16 m, int j) {
-  return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];
-}
 typedef unsigned KoMask8 __attribute__((ext_vector_type(8)));  // 4 masks, s_load_dwordx8
 __device__ __forceinline__ unsigned long long ko_pair8(KoMask8 m, int j) {
   return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];

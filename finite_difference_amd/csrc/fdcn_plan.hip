@@ -60,24 +60,55 @@ void parallel_for(int64_t n, int64_t grain, F f) {
   for (auto& x : th) x.join();
 }
 
-// first j in [lo, hi) with s[j] > x  (bisect.bisect_right)
-int64_t upper(const double* s, int64_t lo, int64_t hi, double x) {
+// bisections over a grid evaluated on demand (s(i) -> node i):
+// first j in [lo, hi) with s(j) > x (bisect.bisect_right) ...
+template <class G>
+int64_t upper_g(const G& s, int64_t lo, int64_t hi, double x) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (x < s[mid]) hi = mid;
+    if (x < s(mid)) hi = mid;
     else lo = mid + 1;
   }
   return lo;
 }
-// first j in [lo, hi) with s[j] >= x  (bisect.bisect_left / searchsorted left)
-int64_t lower(const double* s, int64_t lo, int64_t hi, double x) {
+// ... and first j in [lo, hi) with s(j) >= x (bisect_left / searchsorted left)
+template <class G>
+int64_t lower_g(const G& s, int64_t lo, int64_t hi, double x) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (s[mid] < x) lo = mid + 1;
+    if (s(mid) < x) lo = mid + 1;
     else hi = mid;
   }
   return lo;
 }
+
+// A log grid's nodes, s_i = exp(x_min + i dx) (_build_log_grid), evaluated
+// only where they are read: the payoff max(+-(s_i - K), 0) is exactly 0 on
+// the nodes whose x_i lies clearly on the out-of-the-money side of log K
+// (|x_i - log K| > 1e-9: exp's error, ~1e-16 relative, cannot cross K), so
+// those nodes take no exp -- half the grid on average, and the exps are
+// most of the plan builder's time.  Nodes that are evaluated use the same
+// expression as a full evaluation, so every value is bit-identical.
+struct LogGrid {
+  double x_min, dx;
+  double x(int64_t i) const { return x_min + (double)i * dx; }
+  double operator()(int64_t i) const { return ::exp(x(i)); }
+  // payoff on nodes [0, n): max(s_i - K, 0) (call) / max(K - s_i, 0) (put)
+  void payoff(bool call, double K, int64_t n, double* v) const {
+    const double lk = ::log(K), eps = 1e-9;
+    int64_t a = 0, b = n;  // nodes [a, b) may be in the money
+    if (call) {
+      while (a < n && x(a) < lk - eps) v[a++] = 0.0;
+    } else {
+      while (b > 0 && x(b - 1) > lk + eps) v[--b] = 0.0;
+    }
+    for (int64_t i = a; i < b; ++i) {
+      const double s = (*this)(i);
+      const double e = call ? s - K : K - s;
+      v[i] = (0.0 > e) ? 0.0 : e;  // Python max(e, 0.0)
+    }
+  }
+};
 
 }  // namespace
 
@@ -172,8 +203,7 @@ int fdcn_barrier_plan(int32_t R, const double* row, const int32_t* rflag, double
     // _build_log_grid (:342-364): x_i = x_min + i dx, s_i = exp(x_i), i = 0..N
     const double x_min = ::log(S_min), x_max = ::log(S_max);
     const double dx = (x_max - x_min) / N;
-    std::vector<double> s((size_t)N + 1);
-    for (int32_t i = 0; i <= N; ++i) s[i] = ::exp(x_min + (double)i * dx);
+    const LogGrid s{x_min, dx};  // nodes evaluated where read
     // operator coefficients (…pricer.py:463-472)
     const double sig2 = sigma * sigma;
     const double mu_x = (carry - divy) - 0.5 * sig2;
@@ -190,7 +220,7 @@ int fdcn_barrier_plan(int32_t R, const double* row, const int32_t* rflag, double
     // _boundary_values (:372-393): call top S_max e^{(b-r)tau} - K e^{-r tau};
     // put bottom K e^{-r tau} S_min e^{(b-r) tau} (the :391 product)
     if (call) {
-      P[FDCN_P_HI_C0] = s[N];
+      P[FDCN_P_HI_C0] = s(N);
       P[FDCN_P_HI_E0] = carry - rr;
       P[FDCN_P_HI_C1] = -K;
       P[FDCN_P_HI_E1] = -rr;
@@ -198,13 +228,13 @@ int fdcn_barrier_plan(int32_t R, const double* row, const int32_t* rflag, double
       I[FDCN_I_LO_FORM] = 1;
       P[FDCN_P_LO_C0] = K;
       P[FDCN_P_LO_E0] = -rr;
-      P[FDCN_P_LO_C1] = s[0];
+      P[FDCN_P_LO_C1] = s(0);
       P[FDCN_P_LO_E1] = carry - rr;
     }
     // knock-out thresholds over nodes 0..N-1 (_ko_thresholds)
     int32_t ko_lo = -1, ko_hi = N;
-    if ((kind == 1 || kind == 3) && has_lo) ko_lo = (int32_t)upper(s.data(), 0, N, Hlo) - 1;
-    if ((kind == 2 || kind == 3) && has_up) ko_hi = (int32_t)lower(s.data(), 0, N, Hup);
+    if ((kind == 1 || kind == 3) && has_lo) ko_lo = (int32_t)upper_g(s, 0, N, Hlo) - 1;
+    if ((kind == 2 || kind == 3) && has_up) ko_hi = (int32_t)lower_g(s, 0, N, Hup);
     I[FDCN_I_KO_LO] = std::max(-1, std::min(ko_lo, N));
     I[FDCN_I_KO_HI] = std::max(-1, std::min(ko_hi, N + 1));
     I[FDCN_I_MON_START] = (int32_t)(q * n_mon);
@@ -215,11 +245,7 @@ int fdcn_barrier_plan(int32_t R, const double* row, const int32_t* rflag, double
       mon_rebate[q * n_mon + m] =
           rebate_at_hit ? reb : reb * ::exp(-carry * ((double)mon_k[m] * dt));
     // payoff on nodes 0..N-1 (_terminal_payoff, Python max(e, 0.0))
-    double* v = v_init + q * (int64_t)N;
-    for (int32_t i = 0; i < N; ++i) {
-      const double e = call ? s[i] - K : K - s[i];
-      v[i] = (0.0 > e) ? 0.0 : e;
-    }
+    s.payoff(call, K, N, v_init + q * (int64_t)N);
     // readouts (_interp_price :629-646 at spot - pv; _delta_gamma_from_grid
     // :949-978 at spot, base grid only), on the full grid s[0..N]
     int32_t* ri_ = rint + q * FDCN_GK_NRINT;
@@ -227,34 +253,34 @@ int fdcn_barrier_plan(int32_t R, const double* row, const int32_t* rflag, double
     for (int k = 0; k < FDCN_GK_NRDBL; ++k) rd[k] = 0.0;
     const double S0 = spot - pv;
     ri_[0] = (int32_t)q;  // the solve's index; the caller maps it to a slot
-    if (S0 <= s[0]) {
+    if (S0 <= s(0)) {
       ri_[1] = 1;
       ri_[2] = 0;
-    } else if (S0 >= s[N]) {
+    } else if (S0 >= s(N)) {
       ri_[1] = 2;
       ri_[2] = N - 1;  // V[-1] of the N-node vector
     } else {
-      const int64_t hi = upper(s.data(), 0, N + 1, S0);
+      const int64_t hi = upper_g(s, 0, N + 1, S0);
       ri_[1] = 0;
       ri_[2] = (int32_t)(hi - 1);
-      rd[1] = s[hi - 1];
-      rd[2] = s[hi];
+      rd[1] = s(hi - 1);
+      rd[2] = s(hi);
     }
     rd[0] = S0;
     if (!bump) {
       // 1 + argmin_{1 <= i <= N-1} |s_i - spot| (first on ties)
       int64_t lo_i = 1, hi_i = N - 1;
-      int64_t j = lower(s.data(), lo_i, hi_i + 1, spot);
+      int64_t j = lower_g(s, lo_i, hi_i + 1, spot);
       int64_t idx;
       if (j <= lo_i) idx = lo_i;
       else if (j > hi_i) idx = hi_i;
-      else idx = (::fabs(s[j - 1] - spot) <= ::fabs(s[j] - spot)) ? j - 1 : j;
+      else idx = (::fabs(s(j - 1) - spot) <= ::fabs(s(j) - spot)) ? j - 1 : j;
       ri_[3] = (int32_t)idx;
       ri_[4] = 1;
       rd[3] = spot;
-      rd[4] = s[idx - 1];
-      rd[5] = s[idx];
-      rd[6] = s[idx + 1];
+      rd[4] = s(idx - 1);
+      rd[5] = s(idx);
+      rd[6] = s(idx + 1);
     } else {
       ri_[3] = 0;
       ri_[4] = 0;
@@ -303,23 +329,31 @@ int fdcn_american_plan(int32_t J, const double* job, const int32_t* call, int32_
     // _build_log_grid (:363-384)
     const double x_min = ::log(s_min), x_max = ::log(s_max);
     const double dx = (x_max - x_min) / (double)n;
-    std::vector<double> sv((size_t)n + 1);
-    double* s = s_nodes ? s_nodes + q * (int64_t)(n + 1) : sv.data();
-    for (int32_t i = 0; i <= n; ++i) s[i] = ::exp(x_min + (double)i * dx);
+    // the nodes: all of them when the caller wants the grids (dividend
+    // jumps, the host path), else evaluated where read (LogGrid)
+    const LogGrid grid{x_min, dx};
+    double* sn = s_nodes ? s_nodes + q * (int64_t)(n + 1) : nullptr;
+    if (sn)
+      for (int32_t i = 0; i <= n; ++i) sn[i] = grid(i);
+    auto s = [&](int64_t i) { return sn ? sn[i] : grid(i); };
     // _snap_critical_levels_to_grid (:386-407): argmin |s - x|, first on ties
     auto nearest = [&](double x) -> int32_t {
-      const int64_t j = lower(s, 0, (int64_t)n + 1, x);
+      const int64_t j = lower_g(s, 0, (int64_t)n + 1, x);
       if (j <= 0) return 0;
       if (j > n) return n;
-      return (::fabs(s[j - 1] - x) <= ::fabs(s[j] - x)) ? (int32_t)(j - 1) : (int32_t)j;
+      return (::fabs(s(j - 1) - x) <= ::fabs(s(j) - x)) ? (int32_t)(j - 1) : (int32_t)j;
     };
     const int32_t is = nearest(spot), ik = nearest(K);
-    const double s0 = s[is], ks = s[ik];
+    const double s0 = s(is), ks = s(ik);
     // payoff with the snapped strike (Python max(e, 0.0))
     double* pf = payoff + q * (int64_t)(n + 1);
-    for (int32_t i = 0; i <= n; ++i) {
-      const double e = is_call ? s[i] - ks : ks - s[i];
-      pf[i] = (0.0 > e) ? 0.0 : e;
+    if (sn) {
+      for (int32_t i = 0; i <= n; ++i) {
+        const double e = is_call ? sn[i] - ks : ks - sn[i];
+        pf[i] = (0.0 > e) ? 0.0 : e;
+      }
+    } else {
+      grid.payoff(is_call, ks, n + 1, pf);
     }
     // operator coefficients (q = 0: discrete dividends are jumps)
     const double sig2 = sig * sig;
@@ -334,7 +368,7 @@ int fdcn_american_plan(int32_t J, const double* job, const int32_t* call, int32_
     // Dirichlet values (:430-448): call top s_N e^{(b-r)tau} - K e^{-r tau};
     // put bottom K e^{-r tau}
     if (is_call) {
-      P[FDCN_P_HI_C0] = s[n];
+      P[FDCN_P_HI_C0] = s(n);
       P[FDCN_P_HI_E0] = b - r;
       P[FDCN_P_HI_C1] = -ks;
       P[FDCN_P_HI_E1] = -r;
@@ -355,18 +389,18 @@ int fdcn_american_plan(int32_t J, const double* job, const int32_t* call, int32_
       double* rd = rdbl + (2 * q + c) * FDCN_GK_NRDBL;
       for (int k = 0; k < FDCN_GK_NRDBL; ++k) rd[k] = 0.0;
       ri[0] = (int32_t)q;
-      if (s0 <= s[0]) {
+      if (s0 <= s(0)) {
         ri[1] = 1;
         ri[2] = 0;
-      } else if (s0 >= s[n]) {
+      } else if (s0 >= s(n)) {
         ri[1] = 2;
         ri[2] = n;
       } else {
-        const int64_t hi = upper(s, 0, (int64_t)n + 1, s0);
+        const int64_t hi = upper_g(s, 0, (int64_t)n + 1, s0);
         ri[1] = 0;
         ri[2] = (int32_t)(hi - 1);
-        rd[1] = s[hi - 1];
-        rd[2] = s[hi];
+        rd[1] = s(hi - 1);
+        rd[2] = s(hi);
       }
       rd[0] = s0;
       if (c == 0) {
@@ -378,7 +412,7 @@ int fdcn_american_plan(int32_t J, const double* job, const int32_t* call, int32_
         ri[3] = i;
         ri[4] = 2;
         rd[3] = s0;
-        for (int k = 0; k < 4; ++k) rd[4 + k] = s[i - 1 + k];
+        for (int k = 0; k < 4; ++k) rd[4 + k] = s(i - 1 + k);
       }
     }
     double* g = gout + q * FDCN_AP_NOUT;

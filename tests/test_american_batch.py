@@ -74,8 +74,13 @@ def test_result_rows_match_runner_schema(tmp_path):
         assert df["model_vega"].iloc[i] == g["vega"]
 
 
-def test_plan_bitwise_equal_facade():
-    base = _base("call", n=50)
+@pytest.mark.parametrize("with_grids", [True, False], ids=["grids", "lazy_nodes"])
+@pytest.mark.parametrize("opt", ["call", "put"])
+def test_plan_bitwise_equal_facade(opt, with_grids):
+    """fdcn_american_plan against the facade, bit for bit: with the grids
+    returned (every node evaluated) and without (nodes evaluated where read,
+    the payoff's out-of-the-money side written as zeros without an exp)."""
+    base = _base(opt, n=50)
     rows = _rows(6, 5)
     jobs, calls, solves, reads = [], [], [], []
     for q, r in enumerate(rows):
@@ -84,14 +89,14 @@ def test_plan_bitwise_equal_facade():
         sv = p._segment_solve(p._payoff_array(), 0.0, p.time_to_expiry, p.num_time_steps, True)
         solves.append(sv)
         jobs.append((p.spot, p.strike, p.sigma, p.carry_rate_nacc, p.discount_rate_nacc))
-        calls.append(1)
+        calls.append(1 if opt == "call" else 0)
         s = p.s_nodes
         i = int(np.argmin(np.abs(np.asarray(s) - p.spot_snapped)))
         i = 1 if i < 1 else (len(s) - 3 if i > len(s) - 3 else i)
         reads += [readout(q, s, p.spot_snapped),
                   readout(q, s, p.spot_snapped, p.spot_snapped, dg_mode=2, idx=i)]
         T, smm = p.time_to_expiry, p.s_max_mult
-    plan = capi.american_plan(np.array(jobs), np.array(calls), 50, smm, T, with_grids=True)
+    plan = capi.american_plan(np.array(jobs), np.array(calls), 50, smm, T, with_grids=with_grids)
     g = pack(solves, list(range(len(solves))))
     P = plan["params"].copy()
     P[:, capi.P_DT] = g.params[:, capi.P_DT]

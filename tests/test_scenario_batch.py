@@ -96,12 +96,15 @@ def test_empty_file():
     assert scenario_batch.run_rows_vectorized([], base, oracle_engine()) == []
 
 
+@pytest.mark.parametrize("opt", ["put", "call"])
 @pytest.mark.parametrize("mode", ["parity", "explicit"])
-def test_plan_arrays_bitwise_equal_facade(mode):
-    """The C plan builder against _make_solve + pack + session.readout."""
+def test_plan_arrays_bitwise_equal_facade(mode, opt):
+    """The C plan builder against _make_solve + pack + session.readout (its
+    grid nodes evaluated where read, the payoff's out-of-the-money side
+    written as zeros without an exp: bit for bit, calls and puts)."""
     from finite_difference_amd.barrier import KI_TO_KO, tail_quantile
     from finite_difference_amd.session import readout
-    base = scenarios.runner_base_params("put", 64)
+    base = scenarios.runner_base_params(opt, 64)
     base.update(num_time_steps=48, grid_mode=mode, rebate_amount=0.75, rebate_at_hit=False,
                 divs=[(dt.date(2025, 8, 12), 1.0)])
     rows = [r for r in _rows(12, 11) if r["barrier_type"] != "none"]
@@ -123,7 +126,8 @@ def test_plan_arrays_bitwise_equal_facade(mode):
         row[j] = (r["S0"], r["K"], r["sigma"], r["lower_barrier"] or 0.0,
                   r["upper_barrier"] or 0.0, p.carry_rate_nacc, p.div_yield_nacc,
                   p.discount_rate_nacc, p.pv_divs, 0.75)
-        flag[j] = (1, 1 if bt == "down-and-out" else 2, r["lower_barrier"] is not None,
+        flag[j] = (1 if opt == "put" else 0, 1 if bt == "down-and-out" else 2,
+                   r["lower_barrier"] is not None,
                    r["upper_barrier"] is not None)
         mon = np.asarray(sorted(k for k in p._monitor_indices_tau(p.time_to_expiry / 48)
                                 if 1 <= k <= 48), np.int32)
