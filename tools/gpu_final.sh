@@ -30,9 +30,11 @@ timeout -k 10 300 python bench.py --workload spot_vc --n-space 600 --n-time 600 
 # config 4 with N = 2 ranks sharing this GPU over gloo (the N > 1 code path)
 FDCN_SHARE_DEVICE=1 timeout -k 10 300 python bench.py --gpus 2 --workload barrier --total 10000 \
     --backend gloo > $O/bench_barrier_total_2ranks_gloo.json 2> $O/bench_barrier_total_2ranks_gloo.err || exit $?
+# the driver's bench command (--steps 20 --warmup 5): the summary's average
+# over 25 launches carries the one cold first launch at 1/25 weight
 for wl in american barrier double spot_vc; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o $wl -- \
-      python3 bench.py --workload $wl --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_$wl.log 2>&1 || exit $?
+      python3 bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_$wl.log 2>&1 || exit $?
 done
 bash tools/pmc_counters.sh ${TAG}_pmc american barrier double spot_vc || exit $?
 # the launcher path the driver's scaling run uses (one rank here: one GPU)
