@@ -261,6 +261,7 @@ def _device_chunks(eng: Engine, S, p0, spot, K, sig, carry, disc, dv_sigma: floa
         members = _members(job_nt, nts)
         t_plan += time.perf_counter() - t0
         slot = np.full(J, -1, np.int32)
+        g = None
         for seg in range(max(len(segs[nt][2]) for nt in nts)):
             for nt in nts:
                 steps = segs[nt][2]
