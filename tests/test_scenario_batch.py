@@ -172,3 +172,25 @@ def test_vmath_matches_python_math():
     assert all(a == math.log(b) for a, b in zip(capi.vmath(capi.VM_LOG, y), y))
     assert all(a == math.sqrt(b) for a, b in zip(capi.vmath(capi.VM_SQRT, y), y))
     assert all(a == b ** 2 for a, b in zip(capi.vmath(capi.VM_SQUARE, x), x))
+
+
+def test_grids_that_differ_fall_back_to_the_per_row_path(monkeypatch):
+    """A plan whose rows' grids differ in size (the plan builder's "differ"
+    error) makes price_columns decline (None), so run_all_scenarios takes the
+    per-row facades; other plan errors propagate."""
+    base = scenarios.runner_base_params("put", 40)
+    base.update(num_time_steps=40, grid_mode="parity")
+    rows = _rows(6, 5)
+    cols = scenario_batch.rows_to_columns(rows)
+
+    def differ(*a, **k):
+        raise capi.FdcnError("fdcn_barrier_plan: grid sizes differ across rows")
+    monkeypatch.setattr(scenario_batch.capi, "barrier_plan", differ)
+    assert scenario_batch.price_columns(cols, base, oracle_engine()) is None
+    assert scenario_batch.run_rows_vectorized(rows, base, oracle_engine()) is None
+
+    def broken(*a, **k):
+        raise capi.FdcnError("fdcn_barrier_plan: NULL argument")
+    monkeypatch.setattr(scenario_batch.capi, "barrier_plan", broken)
+    with pytest.raises(capi.FdcnError):
+        scenario_batch.price_columns(cols, base, oracle_engine())
