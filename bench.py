@@ -110,6 +110,8 @@ def parse(argv=None):
     ap.add_argument("--n-time", type=int, default=0, help="0: workload default")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pcie-launches", type=int, default=2,
+                    help="launches timed through the host-array ABI (pcie_inclusive; 0: skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the rank spawn / gloo / timing / gather plumbing without "
                          "a GPU (no march; the line is marked dry_run and is not a measurement)")
@@ -560,6 +562,28 @@ def run_rank(args):
     achieved_gbs = bps * node_steps_launch / kernel_s / 1e9
     ctr = load_counters(workload)
 
+    # the PCIe-inclusive rate of the host-array boundary (fdcn_it_batch /
+    # fdcn_cn_batch with NumPy arrays: H2D of the plan, the march, D2H of
+    # v_out): reported beside the line, never its value
+    pcie = None
+    if rank == 0 and world == 1 and args.pcie_launches > 0 and not args.total:
+        host_call = ((lambda: capi.it_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams,
+                                            g.v_init, g.payoff)) if is_it else
+                     (lambda: capi.cn_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams,
+                                            g.v_init, g.mon_step, g.mon_rebate)))
+        host_call()  # warm (allocations, pinned staging)
+        tp0 = time.perf_counter()
+        for _ in range(args.pcie_launches):
+            host_call()
+        pcie_ms = (time.perf_counter() - tp0) / args.pcie_launches * 1e3
+        pcie = {"ms_per_launch": pcie_ms, "node_steps_per_s": node_steps_launch / (pcie_ms * 1e-3),
+                "launches": args.pcie_launches,
+                "bytes_each_way": {"in": int(g.params.nbytes + g.iparams.nbytes + g.v_init.nbytes +
+                                             (g.payoff.nbytes if is_it else 0)),
+                                   "out": int(g.v_init.nbytes)},
+                "note": "host arrays through the C ABI (fdcn_it_batch / fdcn_cn_batch): H2D, "
+                        "march, D2H per launch; value is the HBM-resident rate"}
+
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(g, args.cpu_seconds, res)
@@ -624,6 +648,7 @@ def run_rank(args):
             "valu_issue": valu,
             "value_per_gpu": value / world,
             "kernel_ms_per_launch": kernel_ms,
+            "pcie_inclusive": pcie,
             "kernel": {"name": f"fdcn_march<IT={int(is_it)}>", **plan, "k_cap": k_cap,
                        "src_sha": kernel_src_sha(),
                        "forced": list(fv) if fv[0] else None,
