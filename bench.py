@@ -654,6 +654,9 @@ def run_rank(args):
                        "forced": list(fv) if fv[0] else None,
                        "lib": capi.LIB_PATH if args.lib else None},
             "outputs_finite": finite,
+            # bits of the last launch's v_out: A/B builds of the kernel that
+            # must agree bitwise compare this
+            "out_sha": hashlib.sha256(np.ascontiguousarray(res).tobytes()).hexdigest()[:16],
             "parity": parity,
             "host_build_s": t_build,
             "cpu_baseline": cpu,
