@@ -623,18 +623,9 @@ fdcn_march(KArgs A) {
     const double* vb = A.v_init + (size_t)scen * n_nodes;
     const double v_lo0 = (IT || kTabSplit) ? U(vb[0]) : 0.0;
     const double v_hi0 = (IT || kTabSplit) ? U(vb[n_nodes - 1]) : 0.0;
-    // The previous step's Dirichlet values (lo_p, hi_p) are bitwise the
-    // lane below's lo / hi: step m's previous tau is step m-1's tau in both
-    // modes (tau0 + m dt; within a run t + j delta, and a run's t_next is
-    // the next run's t).  So each step's values are evaluated once and
-    // shifted up one lane; a chunk's first step takes the previous chunk's
-    // last (carried in lo_c / hi_c; v_init's end values before step 0).
-    double lo_c = v_lo0, hi_c = v_hi0;
-    (void)lo_c;
-    (void)hi_c;
     for (int c = 0; c < A.n_pad; c += kStride) {
       const int m = c + hl;
-      double tau = tau0 + (double)(m + 1) * dt;
+      double tau = tau0 + (double)(m + 1) * dt, tp = tau0 + (double)m * dt;
       if (tau_mode == 1) {  // uniform per scenario: the runs overlapping [c, c + kStride)
         for (;;) {
           if (!have_run) break;
@@ -643,37 +634,33 @@ fdcn_march(KArgs A) {
                           ? run.t_next : run.t + (double)(A.n_time - run.k) * run.delta;
           if (m >= run.k && m < run.k + run.len) {
             const int j = m - run.k;
+            tp = run.t + (double)j * run.delta;
             tau = (j + 1 == run.len) ? run.t_next : run.t + (double)(j + 1) * run.delta;
           }
           if (run.k + run.len >= c + kStride) break;  // continues into the next chunk
           have_run = tau_next_run(tc, kc, A.n_pad, dt, run);
         }
       }
-      // every lane evaluates (a paired wave's missing scenario reads scen0's
-      // values) so the shift below runs on the whole wave; only stores are
-      // guarded
+      if (!valid) continue;
+      (void)tp;
       const double lo = bnd_eval(lof, l0, l1, l2, l3, tau), hi = bnd_eval(hif, h0, h1, h2, h3, tau);
-      if constexpr (IT || kTabSplit) {
-        double lo_p = shfl_up1(lo, 1), hi_p = shfl_up1(hi, 1);
-        if (hl == 0) {
-          lo_p = lo_c;
-          hi_p = hi_c;
-        }
-        lo_c = kPair ? (half ? read_lane(lo, 63) : read_lane(lo, 31)) : read_lane(lo, 63);
-        hi_c = kPair ? (half ? read_lane(hi, 63) : read_lane(hi, 31)) : read_lane(hi, 63);
+      if constexpr (IT) {
+        const double lo_p = m == 0 ? v_lo0 : bnd_eval(lof, l0, l1, l2, l3, tp);
+        const double hi_p = m == 0 ? v_hi0 : bnd_eval(hif, h0, h1, h2, h3, tp);
         const double th = m < A.n_ranna ? 1.0 : 0.5;
-        const double c2 = (1.0 - th) / th;  // Phase::c2 (and pl, pu) of this step's theta
-        if (!valid) continue;
-        if constexpr (IT) {
-          bnd[m] = make_double2((th * dt * ca) * fma(c2, lo_p, lo), (th * dt * cc) * fma(c2, hi_p, hi));
-        } else {
-          // Phase::th, pl, pu, c2 of this step's theta (make_phase)
-          const double AL = -th * dt * ca, AU = -th * dt * cc;
-          bnd[m] = make_double2(th * (-AL * fma(c2, lo_p, lo)), th * (-AU * fma(c2, hi_p, hi)));
-          bnd_raw[m] = make_double2(lo, hi);
-        }
+        const double c2 = (1.0 - th) / th;  // Phase::c2, pl, pu for this step's theta
+        bnd[m] = make_double2((th * dt * ca) * fma(c2, lo_p, lo), (th * dt * cc) * fma(c2, hi_p, hi));
+      } else if constexpr (kTabSplit) {
+        // Phase::th, pl, pu, c2 of this step's theta (make_phase)
+        const double lo_p = m == 0 ? v_lo0 : bnd_eval(lof, l0, l1, l2, l3, tp);
+        const double hi_p = m == 0 ? v_hi0 : bnd_eval(hif, h0, h1, h2, h3, tp);
+        const double th = m < A.n_ranna ? 1.0 : 0.5;
+        const double AL = -th * dt * ca, AU = -th * dt * cc;
+        const double c2 = (1.0 - th) / th;
+        bnd[m] = make_double2(th * (-AL * fma(c2, lo_p, lo)), th * (-AU * fma(c2, hi_p, hi)));
+        bnd_raw[m] = make_double2(lo, hi);
       } else {
-        if (valid) bnd[m] = make_double2(lo, hi);
+        bnd[m] = make_double2(lo, hi);
       }
     }
   }
