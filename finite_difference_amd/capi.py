@@ -322,15 +322,28 @@ def sm_extent(n_nodes: int, n_time: int, n_ranna: int, params: np.ndarray) -> in
     return int(rc)
 
 
+def _out_array(out, B: int, n_nodes: int) -> np.ndarray:
+    """v_out: a new array, or the caller's own (C-contiguous float64 [B,
+    n_nodes]) -- a caller that launches repeatedly reuses one buffer instead
+    of paying first-touch page faults on a fresh one per call."""
+    if out is None:
+        return np.empty((B, n_nodes), dtype=np.float64)
+    if (not isinstance(out, np.ndarray) or out.dtype != np.float64 or out.shape != (B, n_nodes)
+            or not out.flags["C_CONTIGUOUS"] or not out.flags["WRITEABLE"]):
+        raise FdcnError(f"out must be a writeable C-contiguous float64 array of shape {(B, n_nodes)}")
+    return out
+
+
 def cn_batch(n_nodes: int, n_time: int, n_ranna: int, params, iparams, v_init, mon_step,
-             mon_rebate) -> np.ndarray:
-    """Host-array European/KO batch solve -> v_out [B, n_nodes]."""
+             mon_rebate, out=None) -> np.ndarray:
+    """Host-array European/KO batch solve -> v_out [B, n_nodes] (into `out`
+    when given)."""
     require_device()
     P, I, V = _f64(params), _i32(iparams), _f64(v_init)
     B = V.shape[0]
     ms = _i32(mon_step if len(mon_step) else [0])
     mr = _f64(mon_rebate if len(mon_rebate) else [0.0])
-    out = np.empty((B, n_nodes), dtype=np.float64)
+    out = _out_array(out, B, n_nodes)
     _check(lib().fdcn_cn_batch(B, n_nodes, n_time, n_ranna, P.ctypes.data_as(_PD),
                                I.ctypes.data_as(_PI), V.ctypes.data_as(_PD), len(mon_step),
                                ms.ctypes.data_as(_PI), mr.ctypes.data_as(_PD),
@@ -339,12 +352,13 @@ def cn_batch(n_nodes: int, n_time: int, n_ranna: int, params, iparams, v_init, m
 
 
 def it_batch(n_nodes: int, n_time: int, n_ranna: int, params, iparams, v_init,
-             payoff) -> np.ndarray:
-    """Host-array American (Ikonen-Toivanen) batch solve -> v_out [B, n_nodes]."""
+             payoff, out=None) -> np.ndarray:
+    """Host-array American (Ikonen-Toivanen) batch solve -> v_out [B, n_nodes]
+    (into `out` when given)."""
     require_device()
     P, I, V, F = _f64(params), _i32(iparams), _f64(v_init), _f64(payoff)
     B = V.shape[0]
-    out = np.empty((B, n_nodes), dtype=np.float64)
+    out = _out_array(out, B, n_nodes)
     _check(lib().fdcn_it_batch(B, n_nodes, n_time, n_ranna, P.ctypes.data_as(_PD),
                                I.ctypes.data_as(_PI), V.ctypes.data_as(_PD),
                                F.ctypes.data_as(_PD), out.ctypes.data_as(_PD)))

@@ -229,3 +229,20 @@ def test_elf_dynamic_names_reads_needed_and_soname():
     torch_rt = capi._torch_hip_runtime()
     if torch_rt:
         assert capi.elf_dynamic_names(torch_rt)["soname"].startswith("libamdhip64.so")
+
+
+def test_out_buffer_validation():
+    """The host-array wrappers' out= must be a writeable C-contiguous float64
+    [B, n_nodes] array; anything else is refused before any launch."""
+    import numpy as np
+    from finite_difference_amd import capi
+    ok = np.empty((3, 5))
+    assert capi._out_array(ok, 3, 5) is ok
+    assert capi._out_array(None, 3, 5).shape == (3, 5)
+    bad = [np.empty((3, 4)), np.empty((3, 5), dtype=np.float32), np.empty((5, 3)).T,
+           [[0.0] * 5] * 3]
+    ro = np.empty((3, 5))
+    ro.flags.writeable = False
+    for b in bad + [ro]:
+        with pytest.raises(capi.FdcnError):
+            capi._out_array(b, 3, 5)

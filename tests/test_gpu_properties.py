@@ -94,3 +94,23 @@ def test_empty_batch():
     out = capi.it_batch(64, 10, 2, np.zeros((0, capi.NPARAM)), np.zeros((0, capi.NIPARAM)),
                         np.zeros((0, 64)), np.zeros((0, 64)))
     assert out.shape == (0, 64)
+
+
+@pytest.mark.parametrize("workload", ["barrier", "american"])
+def test_host_batch_into_callers_buffer(workload):
+    """capi.cn_batch / it_batch with out=: the caller's buffer is filled and
+    returned, bit for bit what a fresh array receives."""
+    import bench
+    builder, _, _, is_it, _ = bench.WORKLOADS[workload]
+    g = builder(6, 256, 100, seed=3)
+    if is_it:
+        call = lambda out=None: capi.it_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams,  # noqa: E731
+                                              g.v_init, g.payoff, out=out)
+    else:
+        call = lambda out=None: capi.cn_batch(g.n_nodes, g.n_time, g.n_ranna, g.params, g.iparams,  # noqa: E731
+                                              g.v_init, g.mon_step, g.mon_rebate, out=out)
+    fresh = call()
+    buf = np.full((g.B, g.n_nodes), np.nan)
+    got = call(buf)
+    assert got is buf
+    assert np.array_equal(buf, fresh)
