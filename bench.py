@@ -473,6 +473,7 @@ def run_rank(args):
             dist.init_process_group("nccl", device_id=torch.device("cuda", bound))
         else:
             dist.init_process_group("gloo")
+        distributed.check_device_binding(bound)  # no two ranks on one GPU unless shared
     if args.force_variant:
         capi.force_variant(*[int(x) for x in args.force_variant.split(",")])
     dev = torch.device("cuda", bound)

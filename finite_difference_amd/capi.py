@@ -30,7 +30,7 @@ P_HI_C0, P_HI_E0, P_HI_C1, P_HI_E1 = 9, 10, 11, 12
 NPARAM = 13
 I_LO_FORM, I_HI_FORM, I_KO_LO, I_KO_HI, I_MON_START, I_MON_COUNT, I_TAU_MODE = range(7)
 NIPARAM = 7
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 EXPORTED = ("fdcn_cn_batch", "fdcn_it_batch", "fdcn_cn_batch_dev", "fdcn_it_batch_dev",
             "fdcn_plan", "fdcn_sm_extent", "fdcn_log_grid", "fdcn_dividend_jump",
@@ -153,6 +153,19 @@ def lib() -> ctypes.CDLL:
                     f"__graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
             _preload_hip_runtime()
             L = ctypes.CDLL(LIB_PATH)
+            # the version first: a stale build (or bench.py --lib pointing at
+            # an older A/B build) fails here with a clear message rather than
+            # with an AttributeError on a symbol it does not export
+            ver = getattr(L, "fdcn_abi_version", None)
+            if ver is None:
+                raise FdcnError(f"{LIB_PATH} exports no fdcn_abi_version: ABI version "
+                                f"mismatch; rebuild")
+            ver.restype = ctypes.c_int
+            ver.argtypes = []
+            got = int(ver())
+            if got != ABI_VERSION:
+                raise FdcnError(f"libfdcn.so ABI version mismatch (library {got}, package "
+                                f"{ABI_VERSION}); rebuild")
             L.fdcn_cn_batch.restype = _I
             L.fdcn_cn_batch.argtypes = [_I, _I, _I, _I, _PD, _PI, _PD, _I, _PI, _PD, _PD]
             L.fdcn_it_batch.restype = _I
@@ -223,8 +236,6 @@ def lib() -> ctypes.CDLL:
             L.fdcn_vc_variant_name.argtypes = [_I, _I, ctypes.c_char_p, _I]
             L.fdcn_vc_forms.restype = _I
             L.fdcn_vc_forms.argtypes = [_I, _I, _I, _I, _PD, _PI]
-            if L.fdcn_abi_version() != ABI_VERSION:
-                raise FdcnError("libfdcn.so ABI version mismatch; rebuild")
             _lib = L
     return _lib
 

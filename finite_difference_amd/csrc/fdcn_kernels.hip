@@ -274,23 +274,44 @@ struct KoMask {
 
 // One scenario's monitoring entries (wave-uniform): the entry of the next
 // knock-out step and the one after it, loaded a monitor step ahead of their
-// use so the scalar-load latency is off the step.
+// use.  kDefer (round 5): the prefetched entry stays in the VGPRs the vector
+// load wrote and is made scalar (v_readfirstlane) only when the next
+// knock-out advances to it -- taken at load time, the readfirstlane made
+// every knock-out step wait out the load's whole latency (s_waitcnt vmcnt(0)
+// right after the load; ~200 cycles a step with config 5's every-step
+// projection) -- and the entries' addresses are VGPRs (with the array bases
+// in SGPRs the compiler spilled them to VGPR lanes and read them back, eight
+// v_readlane a step).  Config 5 (A/B, one box): 16.60 -> 15.14-15.40 ms.
+// Without kDefer (the register-capped config-3 variant, daily monitoring:
+// knock-outs are rare there and the extra live VGPRs cost more than the
+// waits) the entries are made scalar at load time.
+template <bool kDefer>
 struct MonRun {
-  int pos, end, next, pf;
-  double cur, pf_reb;
+  int pos, end, next;
+  double cur;
+  int pf_v;         // st[pos + 1] as loaded (kDefer: a VGPR, the same in every lane)
+  double pf_reb_v;  // rb[pos + 1] as loaded
+  const int32_t* pst;  // kDefer: &st[pos + 1], &rb[pos + 1] (VGPRs)
+  const double* prb;
+  __device__ __forceinline__ int ld_i(const int32_t* p) { return kDefer ? *p : uni_i(*p); }
+  __device__ __forceinline__ double ld_d(const double* p) { return kDefer ? *p : uni(*p); }
   __device__ __forceinline__ void init(const int32_t* st, const double* rb, int start, int count) {
     pos = start;
     end = start + count;
     // entries < 1 never match a step: skip them (the oracle's `while` does)
     while (pos < end && uni_i(st[pos]) < 1) ++pos;
-    next = pf = 0x7fffffff;
-    cur = pf_reb = 0.0;
+    next = 0x7fffffff;
+    cur = 0.0;
+    pf_v = 0x7fffffff;
+    pf_reb_v = 0.0;
+    pst = st + pos + 1;
+    prb = rb + pos + 1;
     if (pos < end) {
       next = uni_i(st[pos]);
       cur = uni(rb[pos]);
       if (pos + 1 < end) {
-        pf = uni_i(st[pos + 1]);
-        pf_reb = uni(rb[pos + 1]);
+        pf_v = ld_i(pst);
+        pf_reb_v = ld_d(prb);
       }
     }
   }
@@ -298,18 +319,28 @@ struct MonRun {
   // the one after it
   __device__ __forceinline__ void advance(const int32_t* st, const double* rb, int step) {
     ++pos;
-    next = pos < end ? pf : 0x7fffffff;
-    cur = pf_reb;
-    if (pos + 1 < end) {
-      pf = uni_i(st[pos + 1]);
-      pf_reb = uni(rb[pos + 1]);
+    next = pos < end ? (kDefer ? uni_i(pf_v) : pf_v) : 0x7fffffff;
+    cur = kDefer ? uni(pf_reb_v) : pf_reb_v;
+    if constexpr (kDefer) {
+      ++pst;
+      ++prb;
+      asm volatile("" : "+v"(pst), "+v"(prb));
+      if (pos + 1 < end) {
+        pf_v = *pst;
+        pf_reb_v = *prb;
+      }
+    } else if (pos + 1 < end) {
+      pf_v = uni_i(st[pos + 1]);
+      pf_reb_v = uni(rb[pos + 1]);
     }
     if (next <= step) {  // entries not strictly increasing: skip (slow path)
       while (pos < end && uni_i(st[pos]) <= step) ++pos;
       next = (pos < end) ? uni_i(st[pos]) : 0x7fffffff;
       cur = (pos < end) ? uni(rb[pos]) : 0.0;
-      pf = (pos + 1 < end) ? uni_i(st[pos + 1]) : 0x7fffffff;
-      pf_reb = (pos + 1 < end) ? uni(rb[pos + 1]) : 0.0;
+      pf_v = (pos + 1 < end) ? ld_i(st + pos + 1) : 0x7fffffff;
+      pf_reb_v = (pos + 1 < end) ? ld_d(rb + pos + 1) : 0.0;
+      pst = st + pos + 1;
+      prb = rb + pos + 1;
     }
   }
 };
@@ -327,6 +358,44 @@ typedef unsigned KoMask8 __attribute__((ext_vector_type(8)));  // 4 masks, s_loa
 __device__ __forceinline__ unsigned long long ko_pair8(KoMask8 m, int j) {
   return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];
 }
+// The reloaded projection, four slots per block: block G's masks are in mcur
+// (loaded by the block before), block G+1's arrive while block G's four
+// exec-masked moves run (s_load_dwordx8 off the row's base with an immediate
+// offset, waited for at the block's end, so every asm output is valid on
+// exit).  sv: the wave's exec, saved once by the caller and restored at the
+// end of each block (the compiler's code between the statements runs on it).
+template <int G, int NB, int NPT>
+__device__ __forceinline__ void ko_blocks(double (&V)[NPT], double rebv, unsigned long long ka,
+                                          unsigned long long sv, KoMask8 mcur) {
+  if constexpr (G < NB) {
+#define FDCN_KO_MOV(j) "s_and_b64 exec, %[m" #j "], %[sv]\n\tv_mov_b64 %[v" #j "], %[rb]\n\t"
+#define FDCN_KO_OPS                                                                  \
+  [v0] "+v"(V[4 * G]), [v1] "+v"(V[4 * G + 1]), [v2] "+v"(V[4 * G + 2]), [v3] "+v"(V[4 * G + 3])
+#define FDCN_KO_INS                                                                     \
+  [rb] "v"(rebv), [sv] "s"(sv), [m0] "s"(ko_pair8(mcur, 0)), [m1] "s"(ko_pair8(mcur, 1)), \
+      [m2] "s"(ko_pair8(mcur, 2)), [m3] "s"(ko_pair8(mcur, 3))
+    if constexpr (G + 1 < NB) {
+      KoMask8 mnxt;
+      asm volatile("s_load_dwordx8 %[mn], %[ga], %[off]\n\t"
+                   FDCN_KO_MOV(0) FDCN_KO_MOV(1) FDCN_KO_MOV(2) FDCN_KO_MOV(3)
+                   "s_mov_b64 exec, %[sv]\n\ts_waitcnt lgkmcnt(0)"
+                   : FDCN_KO_OPS, [mn] "=&s"(mnxt)
+                   : FDCN_KO_INS, [ga] "s"(ka), [off] "i"(32 * (G + 1))
+                   : "memory", "scc");
+      ko_blocks<G + 1, NB, NPT>(V, rebv, ka, sv, mnxt);
+    } else {
+      asm volatile(FDCN_KO_MOV(0) FDCN_KO_MOV(1) FDCN_KO_MOV(2) FDCN_KO_MOV(3)
+                   "s_mov_b64 exec, %[sv]"
+                   : FDCN_KO_OPS
+                   : FDCN_KO_INS
+                   : "scc");
+    }
+#undef FDCN_KO_MOV
+#undef FDCN_KO_OPS
+#undef FDCN_KO_INS
+  }
+}
+
 // Only the one-wave throughput variants reload from NPT = 16 on: the latency
 // variants (several waves, or the single-trade flavour) have a knock-out on
 // the critical path of one trade, where the s_load latency of every monitor
@@ -465,6 +534,33 @@ struct KArgs {
 // LDS doubles for the scan weights of stages 2-5 (forward and backward, 64
 // lanes): Geo::kScanLds variants
 constexpr int kScanLdsDoubles = 4 * 2 * 64;
+
+// Diagnostic builds only (tools/stamp_timeline.py builds with -DFDCN_STAMPS):
+// per-phase s_memtime stamps of the recovery-form march, for the first
+// kStampScen scenarios and kStampSteps steps from kStampStep0, written by lane
+// 0 into the scenario's Rannacher save slice (vsave, read only in steps m <
+// n_ranna) at [step - kStampStep0][16]; slot 15 of the first step row holds
+// the wave's HW_ID and slot 14 its XCC_ID.  The product build compiles no
+// stamp.
+#ifdef FDCN_STAMPS
+constexpr int kStampScen = 64, kStampStep0 = 1024, kStampSteps = 32;
+#define FDCN_STAMP(k)                                                                 \
+  do {                                                                                \
+    if constexpr (kRec) {                                                             \
+      if (scen < kStampScen && stamp_m >= kStampStep0 &&                              \
+          stamp_m < kStampStep0 + kStampSteps) {                                      \
+        const unsigned long long tt_ = __builtin_amdgcn_s_memtime();                  \
+        if (lane == 0)                                                                \
+          A.vsave[(size_t)scen * 64 * NPT + (stamp_m - kStampStep0) * 16 + (k)] =     \
+              __longlong_as_double((long long)tt_);                                   \
+      }                                                                               \
+    }                                                                                 \
+  } while (0)
+#else
+#define FDCN_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
 
 template <int IT, int W, int NPT, int ZG = 0>
 struct Geo {
@@ -1149,6 +1245,8 @@ fdcn_march(KArgs A) {
   // cycles per link against ~4.2 for independent ones (one wave,
   // tools/ubench/fma64_latency.hip), so a chain is split only where the
   // split is cheap.  Per node-step 4 + ~1 FMAs against 6 + the joins.
+  int stamp_m = -1;  // FDCN_STAMPS: the step being stamped
+  (void)stamp_m;
   auto solve_rec = [&](const Phase& p) __attribute__((always_inline)) {
     constexpr int H = NPT / 2, Q = NPT / 4;
     const double fm = p.fm, bm = p.bm;
@@ -1172,6 +1270,7 @@ fdcn_march(KArgs A) {
         if (j < nst_f) w = fma(wf, scan_up(w, 1 << j, lane4), w);
       }
     }
+    FDCN_STAMP(1);
     const double cin = shfl_up1(w, 1);  // lane 0 receives 0
     FDCN_PRIO_LO();
     // forward pass 2 over the first half from the carry (fm_act: 0 on
@@ -1181,6 +1280,7 @@ fdcn_march(KArgs A) {
     for (int k = 1; k < H; ++k) V[k] = fma(fm, V[k - 1], V[k]);
     // the second half, with the backward zero-carry aggregate of nodes
     // H-1..0 alongside
+    FDCN_STAMP(2);
     double y = V[H - 1];
 #pragma unroll
     for (int k = H; k < NPT; ++k) {
@@ -1201,6 +1301,7 @@ fdcn_march(KArgs A) {
         if (j < nst_b) y = fma(wg, scan_dn(y, 1 << j, lane4), y);
       }
     }
+    FDCN_STAMP(3);
     const double cinb = shfl_dn1(y, 1);  // lane 63 receives 0
     FDCN_PRIO_LO();
     // backward pass 2 fused with the update, per node (descending), as in
@@ -1239,6 +1340,7 @@ fdcn_march(KArgs A) {
     }
     rec_upd(0);
     y0c = uc;
+    FDCN_STAMP(4);
   };
 
   // Two-pass solve (kTP, W = 1): both zero-carry passes in place on Wr, the
@@ -1553,7 +1655,7 @@ fdcn_march(KArgs A) {
   (void)sm_covered;
   // monitoring entries: one run per scenario of the wave (mon2: a paired
   // wave's second scenario; an odd batch's missing one has none)
-  MonRun mon, mon2;
+  MonRun<kWavesPerEu<IT, W, NPT, ZG> == 1> mon, mon2;
   mon.init(A.mon_step, A.mon_rebate, 0, 0);
   mon2.init(A.mon_step, A.mon_rebate, 0, 0);
   if constexpr (!IT) {
@@ -1668,8 +1770,28 @@ fdcn_march(KArgs A) {
       bblk[lane] = bnd_cur;
       asm volatile("" ::: "memory");
     }
+    // kRec: each step's broadcast is read one step ahead (bt_pf), so the
+    // step does not open on an LDS wait (its first instructions form the
+    // Dirichlet rhs terms from it)
+    constexpr bool kBndPf = kBndLds && kRec;
+    double2 bt_pf = make_double2(0.0, 0.0);
+    if constexpr (kBndPf) bt_pf = bblk[0];
+    (void)bt_pf;
     const int m_end = min(m0 + kStride, A.n_time);
   for (int m = m0; m < m_end; ++m) {
+#ifdef FDCN_STAMPS
+    stamp_m = m;
+    if constexpr (kRec) {
+      if (scen < kStampScen && m == kStampStep0 && lane == 0) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        A.vsave[(size_t)scen * 64 * NPT + 15] = (double)hw;
+        A.vsave[(size_t)scen * 64 * NPT + 14] = (double)xcc;
+      }
+    }
+#endif
+    FDCN_STAMP(0);
     if (m == A.n_ranna && use_r) {  // Rannacher -> Crank-Nicolson
       if constexpr (kPair) {
         // reloaded rather than kept live through the march (VGPRs, per lane)
@@ -1692,7 +1814,13 @@ fdcn_march(KArgs A) {
     // kSplit: the tabulated rhs terms; kPair: each scenario's from its own lanes
     double lo_new, hi_new;
     if constexpr (kBndLds) {
-      const double2 bt = bblk[m - m0];
+      double2 bt;
+      if constexpr (kBndPf) {
+        bt = bt_pf;
+        bt_pf = bblk[(m + 1 - m0) & 63];  // the block's last step reads a stale entry, unused
+      } else {
+        bt = bblk[m - m0];
+      }
       lo_new = bt.x;
       hi_new = bt.y;
     } else {  // kPair: each scenario's from its own lanes
@@ -1975,9 +2103,13 @@ fdcn_march(KArgs A) {
     // previous group's arithmetic.
     static_assert(NPT % 4 == 0, "variants need NPT divisible by 4");
     const bool do_sm = (W == 1) || (lz > 64) || (wave == 0);
+    // kRec: the correction only changes nodes of lanes < lz; on a knock-out
+    // step whose lower side removes all of them the projection overwrites it
+    // with the rebate, so it is skipped (config 5 knocks out on every step)
+    const bool sm_skip = kRec && sm_covered && (m + 1 == mon.next);
     double g = 0.0;
     int zoff = 0;
-    if (do_sm) {
+    if (do_sm && !sm_skip) {
       double y0;
       if constexpr (kPair) {
         y0 = bcast_first(Out(0));
@@ -2009,10 +2141,6 @@ fdcn_march(KArgs A) {
     if constexpr (IT || kRec) __builtin_amdgcn_s_setprio(1);
     const double cq = (m + 1 < A.n_ranna) ? 1.0 : 2.0;  // 1/theta of the next step (IT)
     (void)cq;
-    // kRec: the correction only changes nodes of lanes < lz; on a knock-out
-    // step whose lower side removes all of them the projection overwrites it
-    // with the rebate, so it is skipped (config 5 knocks out on every step)
-    const bool sm_skip = kRec && sm_covered && (m + 1 == mon.next);
     if (!sm_skip) {
       const int poff = opaque(kPhiLds ? t : s_t + 1);
       auto phi_at = [&](int k) -> double {
@@ -2101,6 +2229,7 @@ fdcn_march(KArgs A) {
     }
     const bool hit1 = !IT && m + 1 == mon.next;
     const bool hit2 = kPair && m + 1 == mon2.next;  // a paired wave's second scenario
+    FDCN_STAMP(5);
     if (hit1 || hit2) {  // knock-out projection (uniform branch)
       const double reb = kPair ? (half ? mon2.cur : mon.cur) : mon.cur;
       double rebv = reb;  // VGPR copy: v_cndmask takes the mask as its SGPR operand
@@ -2124,44 +2253,16 @@ fdcn_march(KArgs A) {
         asm volatile("" : "+s"(ka));
         // four slots per block, double-buffered (s_load_dwordx8: 16 SGPRs
         // for both buffers; eight-slot blocks held 32 and pushed other
-        // uniform values out to VGPR lanes, read back every step)
+        // uniform values out to VGPR lanes, read back every step).  Round
+        // 5: the blocks' addresses as immediate offsets off one base and
+        // exec saved once per projection (ko_blocks): 8 -> 5 SALU per block
         KoMask8 mcur;
         asm volatile("s_load_dwordx8 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)"
                      : "=s"(mcur)
                      : "s"(ka)
                      : "memory");
-#pragma unroll
-        for (int g = 0; g < NPT / 4; ++g) {
-          KoMask8 mnxt;
-          const bool more = g + 1 < NPT / 4;
-          unsigned long long sv;
-#define FDCN_KO_MOV(j) "s_and_b64 exec, %[m" #j "], %[sv]\n\tv_mov_b64 %[v" #j "], %[rb]\n\t"
-#define FDCN_KO_OPS                                                                  \
-  [v0] "+v"(V[4 * g]), [v1] "+v"(V[4 * g + 1]), [v2] "+v"(V[4 * g + 2]),             \
-      [v3] "+v"(V[4 * g + 3]), [sv] "=&s"(sv)
-#define FDCN_KO_INS                                                                     \
-  [rb] "v"(rebv), [m0] "s"(ko_pair8(mcur, 0)), [m1] "s"(ko_pair8(mcur, 1)),              \
-      [m2] "s"(ko_pair8(mcur, 2)), [m3] "s"(ko_pair8(mcur, 3))
-          if (more) {
-            asm volatile("s_mov_b64 %[sv], exec\n\ts_load_dwordx8 %[mn], %[ga], 0\n\t"
-                         FDCN_KO_MOV(0) FDCN_KO_MOV(1) FDCN_KO_MOV(2) FDCN_KO_MOV(3)
-                         "s_mov_b64 exec, %[sv]\n\ts_waitcnt lgkmcnt(0)"
-                         : FDCN_KO_OPS, [mn] "=&s"(mnxt)
-                         : FDCN_KO_INS, [ga] "s"(ka + 32ull * (g + 1))
-                         : "memory", "scc");
-          } else {
-            asm volatile("s_mov_b64 %[sv], exec\n\t"
-                         FDCN_KO_MOV(0) FDCN_KO_MOV(1) FDCN_KO_MOV(2) FDCN_KO_MOV(3)
-                         "s_mov_b64 exec, %[sv]"
-                         : FDCN_KO_OPS
-                         : FDCN_KO_INS
-                         : "scc");
-          }
-#undef FDCN_KO_MOV
-#undef FDCN_KO_OPS
-#undef FDCN_KO_INS
-          if (more) mcur = mnxt;
-        }
+        const unsigned long long sv = __builtin_amdgcn_read_exec();
+        ko_blocks<0, NPT / 4, NPT>(V, rebv, ka, sv, mcur);
       } else {
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
@@ -2198,6 +2299,7 @@ fdcn_march(KArgs A) {
         else
           ko_prev = kbits(ko_lo, ko_hi);
       }
+      FDCN_STAMP(6);
       if (hit1) mon.advance(A.mon_step, A.mon_rebate, m + 1);
       if (kPair && hit2) mon2.advance(A.mon_step, A.mon_rebate, m + 1);
     }
@@ -2210,6 +2312,7 @@ fdcn_march(KArgs A) {
       halo_l = shfl_up1(shrt ? V[NPT - 2] : V[NPT - 1], 1);
       halo_r = shfl_dn1(V[0], 1);
     }
+    FDCN_STAMP(7);
   }  // step
   }  // block of kStride steps
 

@@ -91,7 +91,44 @@ def bind_device() -> Optional[int]:
             torch.cuda.set_device(dev)
     except ImportError:  # pragma: no cover - torch is always present here
         pass
+    if is_initialized():  # bound after the group formed (the scenario runners)
+        check_device_binding(dev)
     return dev
+
+
+_VISIBLE_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+
+
+def check_device_binding(dev: Optional[int]) -> None:
+    """Collective check, once the group exists, that no two ranks of a host
+    march on the same GPU unless they were told to share it.  bind_device
+    accepts a non-empty *_VISIBLE_DEVICES with one visible device as a
+    per-rank assignment, which a job-wide HIP_VISIBLE_DEVICES=0 with several
+    local ranks also looks like.  Every rank reports (host name,
+    its visible-device variables, the HIP ordinal it bound): two equal
+    reports name the same physical device.  The decision is taken on the
+    gathered list, so every rank raises together (none is left waiting in a
+    later collective)."""
+    import socket
+    from . import capi
+    d = _dist()
+    if d is None:
+        return
+    share = os.environ.get("FDCN_SHARE_DEVICE") == "1"
+    me = None if dev is None else (socket.gethostname(),
+                                   tuple(os.environ.get(v, "") for v in _VISIBLE_VARS), int(dev))
+    reports = [None] * d.get_world_size()
+    d.all_gather_object(reports, (me, share))
+    seen = {}
+    for r, (key, sh) in enumerate(reports):
+        if key is None:
+            continue
+        if key in seen and not (sh and reports[seen[key]][1]):
+            raise capi.FdcnError(
+                f"ranks {seen[key]} and {r} both bound HIP device {key[2]} on {key[0]} "
+                f"(visible-device variables {dict(zip(_VISIBLE_VARS, key[1]))}); give each "
+                f"rank its own device or set FDCN_SHARE_DEVICE=1 to share one on purpose")
+        seen.setdefault(key, r)
 
 
 def shard_range(n: int, rank: Optional[int] = None, world: Optional[int] = None) -> range:
@@ -134,17 +171,24 @@ def gather_columns(cols: dict) -> Optional[dict]:
         return cols
     import numpy as np
     rank, world = d.get_rank(), d.get_world_size()
+    # the column schemas first, on every rank, so a mismatch fails every rank
+    # together instead of rank 0 alone after the gather; a rank
+    # with no rows sends an empty dict and is skipped
+    schemas = [None] * world
+    d.all_gather_object(schemas, list(cols))
+    named = [(r, k) for r, k in enumerate(schemas) if k]
+    for r, k in named[1:]:
+        if k != named[0][1]:
+            raise ValueError(f"gather_columns: rank {r} has columns {k}, rank {named[0][0]} "
+                             f"{named[0][1]}")
     parts = [None] * world if rank == 0 else None
     d.gather_object(cols, parts, dst=0)
     if rank != 0:
         return None
-    parts = [p for p in parts if p]  # a rank with no rows sends an empty dict
+    parts = [p for p in parts if p]
     if not parts:
         return {}
     keys = list(parts[0])
-    for i, p in enumerate(parts[1:], 1):
-        if list(p) != keys:
-            raise ValueError(f"gather_columns: part {i} has columns {list(p)}, part 0 {keys}")
     out = {}
     for k in keys:
         vals = [p[k] for p in parts]

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import bisect
 import ctypes
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -112,8 +113,26 @@ def readout(slot: int, s: Sequence[float], S_interp: float, S_dg: Optional[float
                    (float(S_interp), slo, shi, float(S_dg or 0.0)) + nb)
 
 
+class _PinnedView:
+    """Owner of one host_buffer array (its ``.base``): keeps the Session
+    alive, so the pinned memory cannot be recycled while any view of it
+    exists (a traceback holding a plan array past ``with
+    Session()`` kept a view of freed or reused pinned memory)."""
+    __slots__ = ("session", "__array_interface__", "__weakref__")
+
+    def __init__(self, session: "Session", addr: int, n: int):
+        self.session = session
+        self.__array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (addr, False),
+                                    "version": 3}
+
+
 class Session:
-    """One device session (libfdcn fdcn_session); use as a context manager."""
+    """One device session (libfdcn fdcn_session); use as a context manager.
+
+    ``close()`` (and leaving the ``with`` block) destroys the session, unless
+    arrays from ``host_buffer`` are still alive: the destroy then waits until
+    the last of them is dropped (``close_pending``), so a view never outlives
+    the pinned memory it points into."""
 
     def __init__(self):
         self._L = capi.lib()
@@ -122,11 +141,34 @@ class Session:
         h = _V()
         capi._check(self._L.fdcn_session_create(ctypes.byref(h)))
         self._h = h
+        self._live_views = 0
+        self._close_pending = False
 
-    def close(self) -> None:
+    @property
+    def closed(self) -> bool:
+        return getattr(self, "_h", None) is None
+
+    @property
+    def close_pending(self) -> bool:
+        """close() was called while host_buffer views were alive."""
+        return getattr(self, "_close_pending", False) and not self.closed
+
+    def _destroy(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             h, self._h = self._h, None
+            self._close_pending = False
             capi._check(self._L.fdcn_session_destroy(h))
+
+    def close(self) -> None:
+        if getattr(self, "_live_views", 0) > 0:
+            self._close_pending = True  # the last view's finaliser destroys
+            return
+        self._destroy()
+
+    def _view_dropped(self) -> None:
+        self._live_views -= 1
+        if self._live_views == 0 and self._close_pending:
+            self._destroy()
 
     def __enter__(self) -> "Session":
         return self
@@ -136,7 +178,7 @@ class Session:
 
     def __del__(self):  # pragma: no cover - best effort
         try:
-            self.close()
+            self._destroy()
         except Exception:
             pass
 
@@ -144,11 +186,19 @@ class Session:
         """n float64 of the session's pinned host memory (fdcn_session_host_buffer).
         A march whose payoff / v_init lies in it copies it to the device
         without staging, asynchronously: leave it unchanged until the next
-        greeks_raw / fetch, and drop the array before the session closes
-        (the memory is the session's, recycled after close)."""
+        greeks_raw / fetch.  The array (and every view of it) keeps the
+        session alive: a close() before the last one is dropped defers the
+        destroy to that moment (the memory is the session's, recycled after
+        the destroy)."""
+        if self.closed or self.close_pending:
+            raise capi.FdcnError("host_buffer on a closed session")
         p = _V()
-        capi._check(self._L.fdcn_session_host_buffer(self._h, 8 * max(int(n), 1), ctypes.byref(p)))
-        return np.ctypeslib.as_array(ctypes.cast(p, _PD), shape=(max(int(n), 1),))[:int(n)]
+        m = max(int(n), 1)
+        capi._check(self._L.fdcn_session_host_buffer(self._h, 8 * m, ctypes.byref(p)))
+        owner = _PinnedView(self, int(p.value), m)
+        self._live_views += 1
+        weakref.finalize(owner, self._view_dropped)
+        return np.asarray(owner)[:int(n)]
 
     # -- steps ---------------------------------------------------------------
     def march(self, g, v_init_slots: Optional[np.ndarray] = None) -> np.ndarray:

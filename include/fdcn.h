@@ -45,7 +45,11 @@
 extern "C" {
 #endif
 
-#define FDCN_ABI_VERSION 4
+/* 5: fdcn_session_host_buffer, the diagnostics of include/fdcn_diag.h for the
+ * spot-space kernels (fdcn_vc_force_variant / _variant_name / _forms) and the
+ * fdcn_vc workspace contract (+16 doubles per scenario) changed the exported
+ * surface after 4 */
+#define FDCN_ABI_VERSION 5
 
 /* ---- per-scenario fp64 parameters: params[b*FDCN_NPARAM + k] ---------- */
 enum fdcn_param {

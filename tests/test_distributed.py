@@ -90,20 +90,81 @@ def test_two_rank_gloo_one_shard_on_the_fallback(tmp_path):
         assert (got[col].to_numpy() == ref[col].to_numpy()).all(), col
 
 
+class _FakeDist:
+    """Rank `rank` of a `world`-rank group whose other ranks contribute
+    `others` to every all_gather_object / gather_object."""
+
+    def __init__(self, rank, world, others):
+        self.rank, self.world, self.others = rank, world, others
+        self.gathers = 0
+
+    def get_rank(self):
+        return self.rank
+
+    def get_world_size(self):
+        return self.world
+
+    def all_gather_object(self, out, obj):
+        for r in range(self.world):
+            out[r] = obj if r == self.rank else self.others[r]
+
+    def gather_object(self, obj, out, dst=0):
+        self.gathers += 1
+        if out is not None:
+            self.all_gather_object(out, obj)
+
+
 def test_gather_columns_rejects_mismatched_parts(monkeypatch):
-    class FakeDist:
-        def get_rank(self):
-            return 0
+    """the schema check is collective -- every rank raises, before
+    the gather, not rank 0 alone after it."""
+    for rank in (0, 1):
+        fake = _FakeDist(rank, 2, {0: ["a", "b"], 1: ["b", "a"]})
+        monkeypatch.setattr(fdist, "_dist", lambda: fake)
+        with pytest.raises(ValueError):
+            fdist.gather_columns({"a": [1], "b": [2]} if rank == 0 else {"b": [1], "a": [2]})
+        assert fake.gathers == 0
+    # a rank with no rows (empty schema) is not a mismatch
+    fake = _FakeDist(1, 2, {0: ["a", "b"]})
+    monkeypatch.setattr(fdist, "_dist", lambda: fake)
+    assert fdist.gather_columns({}) is None
 
-        def get_world_size(self):
-            return 2
 
-        def gather_object(self, obj, out, dst=0):
-            out[0] = obj
-            out[1] = {"b": [1], "a": [2]}
-    monkeypatch.setattr(fdist, "_dist", lambda: FakeDist())
-    with pytest.raises(ValueError):
-        fdist.gather_columns({"a": [1], "b": [2]})
+def test_check_device_binding_refuses_two_ranks_on_one_gpu(monkeypatch):
+    """a job-wide HIP_VISIBLE_DEVICES=0 with two local ranks makes
+    both bind the one device; the collective check raises on every rank.
+    Distinct per-rank visible sets, distinct ordinals or FDCN_SHARE_DEVICE=1
+    on both ranks pass."""
+    import socket
+    from finite_difference_amd import capi
+    host = socket.gethostname()
+    for v in ("ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "FDCN_SHARE_DEVICE"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+
+    def report(vis, dev, share=False):
+        return ((host, (vis, "", ""), dev), share)
+    for rank in (0, 1):
+        fake = _FakeDist(rank, 2, {0: report("0", 0), 1: report("0", 0)})
+        monkeypatch.setattr(fdist, "_dist", lambda: fake)
+        with pytest.raises(capi.FdcnError):
+            fdist.check_device_binding(0)
+    fake = _FakeDist(0, 2, {1: report("1", 0)})  # per-rank sets "0" / "1"
+    monkeypatch.setattr(fdist, "_dist", lambda: fake)
+    fdist.check_device_binding(0)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    fake = _FakeDist(0, 2, {1: report("", 1)})  # two visible devices, ordinals 0 / 1
+    monkeypatch.setattr(fdist, "_dist", lambda: fake)
+    fdist.check_device_binding(0)
+    monkeypatch.setenv("FDCN_SHARE_DEVICE", "1")
+    fake = _FakeDist(0, 2, {1: report("", 0, True)})  # shared on purpose
+    monkeypatch.setattr(fdist, "_dist", lambda: fake)
+    fdist.check_device_binding(0)
+    fake = _FakeDist(0, 2, {1: report("", 0, False)})  # only one rank asked to share
+    monkeypatch.setattr(fdist, "_dist", lambda: fake)
+    with pytest.raises(capi.FdcnError):
+        fdist.check_device_binding(0)
+    monkeypatch.setattr(fdist, "_dist", lambda: None)
+    fdist.check_device_binding(0)  # no group: nothing to check
 
 
 def test_bind_device_maps_local_rank_through_gfx950_ordinals(monkeypatch):

@@ -1,4 +1,4 @@
-"""The C-ABI boundary's contracts on the MI355X (include/fdcn.h, ABI 4).
+"""The C-ABI boundary's contracts on the MI355X (include/fdcn.h, ABI 5).
 
 * FDCN_I_TAU_MODE = 1 (the reference American loop's accumulated tau,
   fd_american_equity.py:664-724) is honoured on the device;
