@@ -183,6 +183,20 @@ __device__ __forceinline__ double bnd_eval(int form, double c0, double e0, doubl
   if (form == 1) return c0 * exp(e0 * tau) * c1 * exp(e1 * tau);
   return c0 * exp(e0 * tau) + c1 * exp(e1 * tau);
 }
+// The same value, bitwise, without the exp of a term whose coefficient is
+// zero (wave-uniform branches): c * exp(y) is c itself for c = +-0 and a
+// finite exp(y).  A call's lower and a put's upper Dirichlet value are such
+// terms (…pricer.py:381-391).  Used where the evaluation sits in the march
+// (kGen).
+__device__ __forceinline__ double bnd_eval_nz(int form, double c0, double e0, double c1,
+                                              double e1, double tau) {
+  const double t0 = c0 == 0.0 ? c0 : c0 * exp(e0 * tau);
+  if (form == 1) {
+    const double p = t0 * c1;
+    return p == 0.0 ? p : p * exp(e1 * tau);
+  }
+  return t0 + (c1 == 0.0 ? c1 : c1 * exp(e1 * tau));
+}
 
 // Uniform per-phase (per theta) constants.
 struct Phase {
@@ -514,7 +528,7 @@ struct KArgs {
   const int32_t* mon_step;
   const double* mon_rebate;
   double* v_out;
-  double* bnd;      // workspace: Dirichlet terms [B][W][n_pad + kKoRow (+ n_pad split form)][2]
+  double* bnd;      // workspace: [B][W][n_pad Dirichlet terms (not rec_form) + kKoRow masks (+ n_pad raw split form)][2]
   double* zg;       // workspace: correction tables [B][2][lz][NPT+1] (ZG variants)
   double* vsave;    // workspace: old V of a Rannacher step [B][64][NPT] (rec_form variants)
   int n_pad;        // n_time rounded up to a multiple of 64
@@ -674,90 +688,140 @@ fdcn_march(KArgs A) {
   const double cbc = U(P[FDCN_P_BC]);
   const double tau0 = U(P[FDCN_P_TAU0]);
 
-  // Dirichlet values of every step, evaluated once up front (while few
-  // registers are live) into this wave's workspace row: lane l owns steps
-  // m = l (mod 64) and is the only lane that reads them back, so no
-  // synchronisation is needed.  tau_m = tau0 + (m+1) dt (…pricer.py:519),
-  // or with FDCN_I_TAU_MODE = 1 the reference American loop's accumulated
-  // tau (tau = tau + dt per step, fd_american_equity.py:664-724).
-  // IT: what the step needs is not the Dirichlet value itself but its
-  // theta-form rhs term (-A_L)(lo_m + c2 lo_{m-1}) / (-A_U)(hi_m + c2 hi_{m-1})
-  // (see the IT rhs below); IT has no knock-out, so lo_{m-1} is simply the
-  // previous step's value and the whole term is tabulated here.
+  // Boundary entries.  Step m's Dirichlet values at tau_m = tau0 + (m+1) dt
+  // (…pricer.py:519), or with FDCN_I_TAU_MODE = 1 the reference American
+  // loop's accumulated tau (tau = tau + dt per step,
+  // fd_american_equity.py:664-724).  IT: what the step needs is not the value
+  // itself but its theta-form rhs term (-A_L)(lo_m + c2 lo_{m-1}) /
+  // (-A_U)(hi_m + c2 hi_{m-1}) (see the IT rhs below; IT has no knock-out, so
+  // lo_{m-1} is simply the previous step's value).  The one-wave split-form
+  // CN variants (kTabSplit) use the same term, th (-A_L)(lo_new + c2
+  // lo_prev), with the expression and operand order of the in-loop form it
+  // replaces; a knock-out that removes node 0 or the last node sets lo_prev
+  // / hi_prev to the rebate instead, and the step after one recomputes its
+  // term from the raw values.  Other CN variants take the raw values.
+  // gen(c, raw) evaluates chunk c's entries, one step per lane (lane l: step
+  // c + l), when the march reaches the chunk.  Up to round 4 a prologue
+  // tabulated every step in the workspace and the march read the table back
+  // (16-32 B per step and scenario each way: 0.5-1 GB of HBM traffic per
+  // launch of configs 2, 3 and 5); the values are the same numbers, bitwise.
+  // The boundary parameters are reloaded from `params` at each chunk rather
+  // than kept live through the march.
+  // kGen (the recovery-form variants, config 5): the chunk's entries are
+  // evaluated in the march when it reaches the chunk, so no table crosses
+  // HBM.  The other variants keep the round-4 table, filled by a prologue
+  // (gen over every chunk) and read back per chunk: evaluated in the march
+  // their exp temporaries sit on top of the march's live registers -- IT
+  // (config 2) 245 -> 266 VGPRs (one wave per SIMD), the capped split-form
+  // variant (config 3) 24 -> 128 B of scratch -- while config 5's variant
+  // keeps two waves per SIMD (233 -> 255)
+  constexpr bool kGen = rec_form(IT, W, NPT);
+  constexpr bool kTabSplit = tab_form(IT, W, NPT, (ZG >> 1) & 1);
   double2* bnd = reinterpret_cast<double2*>(A.bnd) +
                  ((size_t)scen * W + wave) *
-                     (A.n_pad + kKoRow + (tab_form(IT, W, NPT, (ZG >> 1) & 1) ? A.n_pad : 0));
-  const int lof = Ui(I[FDCN_I_LO_FORM]), hif = Ui(I[FDCN_I_HI_FORM]);
-  const double l0 = U(P[FDCN_P_LO_C0]), l1 = U(P[FDCN_P_LO_E0]), l2 = U(P[FDCN_P_LO_C1]),
-               l3 = U(P[FDCN_P_LO_E1]);
-  const double h0 = U(P[FDCN_P_HI_C0]), h1 = U(P[FDCN_P_HI_E0]), h2 = U(P[FDCN_P_HI_C1]),
-               h3 = U(P[FDCN_P_HI_E1]);
+                     (kKoRow + (kGen ? 0 : A.n_pad * (kTabSplit ? 2 : 1)));
+  double2* kom_row = bnd + (kGen ? 0 : A.n_pad);
+  double2* bnd_raw = kom_row + kKoRow;  // kTabSplit only
+  (void)bnd_raw;
   const int tau_mode = Ui(I[FDCN_I_TAU_MODE]);
   // steps m = hl (mod L) are this lane's (kStride lanes per scenario)
   constexpr int kStride = kPair ? 32 : 64;
   double tau_end = tau0 + (double)A.n_time * dt;  // tau after the last step
   // tau_mode 1: the runs of the tau sequence (tau_next_run) are walked chunk
-  // by chunk below, each lane picking (tau_{m+1}, tau_m) of its own step from
-  // the runs overlapping the chunk -- no round trip of the tau pairs through
-  // the workspace (2 x 16 B per step and scenario: 2 x 268 MB per config-2
-  // launch), and the boundary values' exp stays outside any divergent branch
+  // by chunk, each lane picking (tau_{m+1}, tau_m) of its own step from the
+  // runs overlapping the chunk, so the exp stays outside any divergent branch
   double tc = tau0;
   int kc = 0;
   TauRun run;
   bool have_run = tau_mode == 1 && tau_next_run(tc, kc, A.n_pad, dt, run);
-  // Split-form CN (kSplit below) tabulates its rhs terms too: th (-A_L)(lo_new
-  // + c2 lo_prev) with lo_prev the previous step's Dirichlet value, the
-  // expression and operand order of the in-loop form it replaces (bitwise the
-  // same numbers).  A knock-out that removes node 0 or the last node sets
-  // lo_prev / hi_prev to the rebate instead: the step after one recomputes
-  // its term from the raw values, kept in a second table (bnd_raw; evaluating
-  // them again in the loop would keep exp's registers live in the march).
-  constexpr bool kTabSplit = tab_form(IT, W, NPT, (ZG >> 1) & 1);
-  double2* bnd_raw = bnd + A.n_pad + kKoRow;  // kTabSplit only
-  (void)bnd_raw;
-  {
-    const double* vb = A.v_init + (size_t)scen * n_nodes;
-    const double v_lo0 = (IT || kTabSplit) ? U(vb[0]) : 0.0;
-    const double v_hi0 = (IT || kTabSplit) ? U(vb[n_nodes - 1]) : 0.0;
-    for (int c = 0; c < A.n_pad; c += kStride) {
-      const int m = c + hl;
-      double tau = tau0 + (double)(m + 1) * dt, tp = tau0 + (double)m * dt;
-      if (tau_mode == 1) {  // uniform per scenario: the runs overlapping [c, c + kStride)
-        for (;;) {
-          if (!have_run) break;
-          if (run.k < A.n_time && A.n_time <= run.k + run.len)
-            tau_end = (A.n_time == run.k + run.len)
-                          ? run.t_next : run.t + (double)(A.n_time - run.k) * run.delta;
-          if (m >= run.k && m < run.k + run.len) {
-            const int j = m - run.k;
-            tp = run.t + (double)j * run.delta;
-            tau = (j + 1 == run.len) ? run.t_next : run.t + (double)(j + 1) * run.delta;
-          }
-          if (run.k + run.len >= c + kStride) break;  // continues into the next chunk
-          have_run = tau_next_run(tc, kc, A.n_pad, dt, run);
+  const double* vb = A.v_init + (size_t)scen * n_nodes;
+  const double v_lo0 = (IT || kTabSplit) ? U(vb[0]) : 0.0;
+  const double v_hi0 = (IT || kTabSplit) ? U(vb[n_nodes - 1]) : 0.0;
+  struct Bnd {  // the boundary parameters of this lane's scenario
+    int lof, hif;
+    double l0, l1, l2, l3, h0, h1, h2, h3, t0;
+  };
+  // (one scenario per wave: scalar loads through the constant address space
+  // -- params / iparams are read-only for the launch -- so no VGPR holds a
+  // loaded value; a paired wave's two scenarios load per lane)
+  auto bnd_params = [&]() __attribute__((always_inline)) {
+    if constexpr (kPair) {
+      const double* Pg = P;
+      const int32_t* Ig = I;
+      asm volatile("" : "+v"(Pg), "+v"(Ig));
+      return Bnd{Ig[FDCN_I_LO_FORM], Ig[FDCN_I_HI_FORM], Pg[FDCN_P_LO_C0], Pg[FDCN_P_LO_E0],
+                 Pg[FDCN_P_LO_C1], Pg[FDCN_P_LO_E1], Pg[FDCN_P_HI_C0], Pg[FDCN_P_HI_E0],
+                 Pg[FDCN_P_HI_C1], Pg[FDCN_P_HI_E1], Pg[FDCN_P_TAU0]};
+    } else {
+      typedef const double __attribute__((address_space(4))) cdbl;
+      typedef const int32_t __attribute__((address_space(4))) cint;
+      const cdbl* Pg = (const cdbl*)(uintptr_t)P;
+      const cint* Ig = (const cint*)(uintptr_t)I;
+      asm volatile("" : "+s"(Pg), "+s"(Ig));
+      return Bnd{Ig[FDCN_I_LO_FORM], Ig[FDCN_I_HI_FORM], Pg[FDCN_P_LO_C0], Pg[FDCN_P_LO_E0],
+                 Pg[FDCN_P_LO_C1], Pg[FDCN_P_LO_E1], Pg[FDCN_P_HI_C0], Pg[FDCN_P_HI_E0],
+                 Pg[FDCN_P_HI_C1], Pg[FDCN_P_HI_E1], Pg[FDCN_P_TAU0]};
+    }
+  };
+  auto gen = [&](int c, double2& raw) __attribute__((always_inline)) -> double2 {
+    const Bnd q = bnd_params();
+    const int m = c + hl;
+    double tau = q.t0 + (double)(m + 1) * dt, tp = q.t0 + (double)m * dt;
+    if (tau_mode == 1) {  // uniform per scenario: the runs overlapping [c, c + kStride)
+      for (;;) {
+        if (!have_run) break;
+        if (run.k < A.n_time && A.n_time <= run.k + run.len)
+          tau_end = (A.n_time == run.k + run.len)
+                        ? run.t_next : run.t + (double)(A.n_time - run.k) * run.delta;
+        if (m >= run.k && m < run.k + run.len) {
+          const int j = m - run.k;
+          tp = run.t + (double)j * run.delta;
+          tau = (j + 1 == run.len) ? run.t_next : run.t + (double)(j + 1) * run.delta;
         }
+        if (run.k + run.len >= c + kStride) break;  // continues into the next chunk
+        have_run = tau_next_run(tc, kc, A.n_pad, dt, run);
       }
-      if (!valid) continue;
-      (void)tp;
-      const double lo = bnd_eval(lof, l0, l1, l2, l3, tau), hi = bnd_eval(hif, h0, h1, h2, h3, tau);
-      if constexpr (IT) {
-        const double lo_p = m == 0 ? v_lo0 : bnd_eval(lof, l0, l1, l2, l3, tp);
-        const double hi_p = m == 0 ? v_hi0 : bnd_eval(hif, h0, h1, h2, h3, tp);
-        const double th = m < A.n_ranna ? 1.0 : 0.5;
-        const double c2 = (1.0 - th) / th;  // Phase::c2, pl, pu for this step's theta
-        bnd[m] = make_double2((th * dt * ca) * fma(c2, lo_p, lo), (th * dt * cc) * fma(c2, hi_p, hi));
-      } else if constexpr (kTabSplit) {
-        // Phase::th, pl, pu, c2 of this step's theta (make_phase)
-        const double lo_p = m == 0 ? v_lo0 : bnd_eval(lof, l0, l1, l2, l3, tp);
-        const double hi_p = m == 0 ? v_hi0 : bnd_eval(hif, h0, h1, h2, h3, tp);
-        const double th = m < A.n_ranna ? 1.0 : 0.5;
-        const double AL = -th * dt * ca, AU = -th * dt * cc;
-        const double c2 = (1.0 - th) / th;
-        bnd[m] = make_double2(th * (-AL * fma(c2, lo_p, lo)), th * (-AU * fma(c2, hi_p, hi)));
-        bnd_raw[m] = make_double2(lo, hi);
-      } else {
-        bnd[m] = make_double2(lo, hi);
-      }
+    }
+    (void)tp;
+    // kGen: the evaluations one after another (each argument made to depend
+    // on the previous result), so their temporaries do not pile up on top of
+    // the march's live registers
+    auto seq = [](double x, double after) __attribute__((always_inline)) {
+      if constexpr (kGen) asm volatile("" : "+v"(x) : "v"(after));
+      return x;
+    };
+    auto ev = [](int f, double c0, double e0, double c1, double e1, double t)
+        __attribute__((always_inline)) {
+      return kGen ? bnd_eval_nz(f, c0, e0, c1, e1, t) : bnd_eval(f, c0, e0, c1, e1, t);
+    };
+    const double lo = ev(q.lof, q.l0, q.l1, q.l2, q.l3, tau);
+    const double hi = ev(q.hif, q.h0, q.h1, q.h2, q.h3, seq(tau, lo));
+    raw = make_double2(lo, hi);
+    if constexpr (IT) {
+      const double lo_p = m == 0 ? v_lo0 : bnd_eval(q.lof, q.l0, q.l1, q.l2, q.l3, seq(tp, hi));
+      const double hi_p = m == 0 ? v_hi0 : bnd_eval(q.hif, q.h0, q.h1, q.h2, q.h3, seq(tp, lo_p));
+      const double th = m < A.n_ranna ? 1.0 : 0.5;
+      const double c2 = (1.0 - th) / th;  // Phase::c2, pl, pu for this step's theta
+      return make_double2((th * dt * ca) * fma(c2, lo_p, lo), (th * dt * cc) * fma(c2, hi_p, hi));
+    } else if constexpr (kTabSplit) {
+      // Phase::th, pl, pu, c2 of this step's theta (make_phase)
+      const double lo_p = m == 0 ? v_lo0 : bnd_eval(q.lof, q.l0, q.l1, q.l2, q.l3, seq(tp, hi));
+      const double hi_p = m == 0 ? v_hi0 : bnd_eval(q.hif, q.h0, q.h1, q.h2, q.h3, seq(tp, lo_p));
+      const double th = m < A.n_ranna ? 1.0 : 0.5;
+      const double AL = -th * dt * ca, AU = -th * dt * cc;
+      const double c2 = (1.0 - th) / th;
+      return make_double2(th * (-AL * fma(c2, lo_p, lo)), th * (-AU * fma(c2, hi_p, hi)));
+    } else {
+      return raw;
+    }
+  };
+  if constexpr (!kGen) {  // the table: every chunk up front, while few registers are live
+    for (int c = 0; c < A.n_pad; c += kStride) {
+      double2 raw;
+      const double2 e = gen(c, raw);
+      if (!valid) continue;  // a paired wave's missing scenario: no stores
+      bnd[c + hl] = e;
+      if constexpr (kTabSplit) bnd_raw[c + hl] = raw;
     }
   }
 
@@ -1606,7 +1670,7 @@ fdcn_march(KArgs A) {
   unsigned long long kom_addr = 0;  // this wave's mask row (KoLoad variants)
   unsigned long long kom_addr2 = 0, kom_addr12 = 0;  // kPair: second scenario's / both
   if constexpr (KoLoad<IT, W, NPT, ZG>::value) {
-    unsigned long long* kom = reinterpret_cast<unsigned long long*>(bnd + A.n_pad);
+    unsigned long long* kom = reinterpret_cast<unsigned long long*>(kom_row);
     // kRec / kSplit keep the phantom slot of short lanes at zero: never knock it out
     const unsigned long long shrt_lanes = (kRec || kSplit) ? (unsigned long long)__ballot(shrt) : 0ull;
     auto slot_mask = [&](const KoMask& ml, const KoMask& mh, int k) {
@@ -1738,13 +1802,16 @@ fdcn_march(KArgs A) {
   smc_l = sm_row * smc;
   s_l = shrt ? 0.0 : ph.s;
 
-  // The register-capped config-3 variant loads each block when it starts:
-  // a prefetched next block spilled to scratch there (16 B per lane and
-  // block out and back in: +170 MB of HBM traffic per launch).
-  constexpr bool kBndPrefetch = kWavesPerEu<IT, W, NPT, ZG> == 1;
-  double2 bnd_cur = make_double2(0.0, 0.0);
+  // The register-capped config-3 variant evaluates each chunk's entries when
+  // it starts; the others evaluate the next chunk's at the start of this one
+  // (their exp latency then overlaps a whole chunk of steps).  (Round 4, with
+  // a table: a prefetched next block spilled to scratch in the capped
+  // variant, +170 MB of HBM traffic per launch.)
+  constexpr bool kBndPrefetch = !kGen && kWavesPerEu<IT, W, NPT, ZG> == 1;
+  double2 bnd_cur = make_double2(0.0, 0.0), raw_cur = make_double2(0.0, 0.0);
   double2 bnd_nxt = kBndPrefetch ? bnd[hl] : make_double2(0.0, 0.0);  // steps 0..kStride-1
   (void)bnd_nxt;
+  (void)raw_cur;
   int ko_prev = 0;  // kSplit: bit 0 / 1 -- the last step knocked out node 0 / the last node
   (void)ko_prev;
   double halo_l = 0.0, halo_r = 0.0;
@@ -1757,7 +1824,9 @@ fdcn_march(KArgs A) {
   // flight.  With the refill inside a flat step loop the compiler rotated the
   // two buffers through copies on every step (8 v_mov_b64 per step).
   for (int m0 = 0; m0 < A.n_time; m0 += kStride) {
-    if constexpr (kBndPrefetch) {
+    if constexpr (kGen) {
+      bnd_cur = gen(m0, raw_cur);
+    } else if constexpr (kBndPrefetch) {
       bnd_cur = bnd_nxt;
       if (m0 + kStride < A.n_pad) bnd_nxt = bnd[m0 + kStride + hl];  // prefetch the block after
     } else {
@@ -2318,8 +2387,9 @@ fdcn_march(KArgs A) {
 
   if constexpr (IT) {  // Dirichlet values of the last step (the loop kept only rhs terms)
     if (A.n_time > 0) {
-      V0 = bnd_eval(lof, l0, l1, l2, l3, tau_end);
-      VN = bnd_eval(hif, h0, h1, h2, h3, tau_end);
+      const Bnd q = bnd_params();
+      V0 = bnd_eval(q.lof, q.l0, q.l1, q.l2, q.l3, tau_end);
+      VN = bnd_eval(q.hif, q.h0, q.h1, q.h2, q.h3, tau_end);
     }
   }
   if constexpr (kTabSplit) {  // likewise, unless the last step knocked the node out
@@ -2488,12 +2558,17 @@ const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
       }
     }
   }
-  // Batches too small to put a wave on every SIMD: the single-trade flavour
-  // of the chosen W = 1 variant (in-wave ILP), compiled for NPT 8-32.
-  // Measured on one trade (bench.py trade_*): config-2 grids 8.42 -> 8.28 ms,
-  // config 1 unchanged; for 64-node chunks (config 5) the split over 4 waves
-  // below wins (12.0 ms against 13.5 for either W = 1 flavour).
-  if (best && best->w == 1 && best->npt < 48 && B * best->w <= kResidentWaves / 2 && !best->zg)
+  // Batches too small to put a wave on every SIMD, IT march only: the
+  // single-trade flavour of the chosen W = 1 variant (in-wave ILP).  Measured
+  // (profiles/r05_small_batch/): trade_american (IT, NPT 32) 8.23 -> 7.47 ms
+  // per trade; but the CN flavour loses everywhere it was timed --
+  // trade_cnlog (NPT 8) 0.426 -> 0.496 ms, the config-3 grid (NPT 16) at
+  // B = 64 / 256 / 512 / 1024: 0.75 / 0.76 / 0.87 / 0.83 ms -> 0.98 / 0.99 /
+  // 1.12 / 1.08 -- so CN keeps one scenario per wave.  For 64-node chunks
+  // (config 5) the split over 4 waves below wins (12.0 ms against 13.5 for
+  // either W = 1 flavour).
+  if (best && it && best->w == 1 && best->npt < 48 && B * best->w <= kResidentWaves / 2 &&
+      !best->zg)
     for (int i = 0; i < kNumVariants; ++i) {
       const Variant& v = kVariants[i];
       if (v.lat && v.it == it && v.w == 1 && v.npt == best->npt && !v.zg) return &v;
@@ -2529,14 +2604,16 @@ int lds_doubles(const Variant& v, int lz) { return v.lds_per_scen(lz) * v.spb; }
 
 int pad64(int n) { return ((n > 0 ? n : 1) + 63) / 64 * 64; }
 
-// workspace bytes per scenario: one (lo, hi) Dirichlet pair per step and
-// wave plus the knock-out mask row (kKoRow) of each wave (split-form
-// variants: a second pair per step, the raw values behind their rhs terms);
-// ZG variants add the correction table [2][lz][NPT+1], rec_form variants
-// the Rannacher save slice [64][NPT]
+// workspace bytes per scenario: per wave, one (lo, hi) Dirichlet pair per
+// step (split-form variants: a second pair, the raw values behind their rhs
+// terms) -- except the rec_form variants, which evaluate each chunk's
+// entries in the march (kGen) -- then the knock-out mask row (kKoRow); ZG
+// variants add the correction table [2][lz][NPT+1], rec_form variants the
+// Rannacher save slice [64][NPT]
 size_t bnd_bytes_per_scen(const Variant& v, int n_time) {
-  const size_t row = (size_t)pad64(n_time) * (tab_form(v.it, v.w, v.npt, v.lat) ? 2 : 1) + kKoRow;
-  return sizeof(double) * 2 * row * (size_t)v.w;
+  const size_t table = rec_form(v.it, v.w, v.npt)
+                           ? 0 : (size_t)pad64(n_time) * (tab_form(v.it, v.w, v.npt, v.lat) ? 2 : 1);
+  return sizeof(double) * 2 * (table + kKoRow) * (size_t)v.w;
 }
 size_t zg_bytes_per_scen(const Variant& v, int lz) {
   return v.zg ? sizeof(double) * 2 * (size_t)lz * (size_t)(v.npt + 1) : 0;

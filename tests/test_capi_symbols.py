@@ -36,11 +36,17 @@ def test_launch_path_reads_no_environment():
 def test_force_variant_pins_and_clears():
     big = capi.variant_name(1024, False, B=10000)
     assert big == "fdcn_march<0,1,16,0>", big
-    assert capi.variant_name(1024, False, B=8) == "fdcn_march<0,1,16,2>"  # single-trade flavour
+    # small batches: the single-trade flavour for the IT march only (the CN
+    # flavour measured slower at every batch size, fdcn_kernels.hip choose())
+    assert capi.variant_name(1024, False, B=8) == big
+    assert capi.variant_name(1024, True, B=8) == "fdcn_march<1,1,16,2>"
     try:
+        capi.force_variant(1, 16, 1)
+        assert capi.forced_variant() == (1, 16, 1)
+        assert capi.variant_name(1024, False, B=8) == "fdcn_march<0,1,16,2>"
         capi.force_variant(1, 16)
         assert capi.forced_variant() == (1, 16, 0)
-        assert capi.variant_name(1024, False, B=8) == big
+        assert capi.variant_name(1024, True, B=8) == "fdcn_march<1,1,16,0>"
         assert capi.plan(1024, False, B=8)["npt"] == 16
         with pytest.raises(capi.FdcnError):
             capi.force_variant(3, 16)  # not compiled
@@ -48,7 +54,7 @@ def test_force_variant_pins_and_clears():
     finally:
         capi.force_variant(0)
     assert capi.forced_variant() == (0, 0, 0)
-    assert capi.variant_name(1024, False, B=8) == "fdcn_march<0,1,16,2>"
+    assert capi.variant_name(1024, True, B=8) == "fdcn_march<1,1,16,2>"
 
 
 def test_library_exports_all_symbols():

@@ -349,3 +349,82 @@ def test_vc_forms_classify_the_reference_rows_pointwise():
         assert forms([base]) == [0]
     finally:
         capi.vc_force_variant(0, 0, False)
+
+
+def _random_rows(sv, seed, alpha, spread):
+    """A copy of `sv` whose implicit rows are random and, in many rows, NOT
+    diagonally dominant: main_i in [1, 2], sub_i / main_i and sup_i / main_i
+    drawn from [-spread, spread] (|sub| + |sup| up to 2 spread |main|); the
+    explicit rows alpha times the implicit off-diagonals plus a random
+    diagonal (the pointwise form's shape).  Both phases."""
+    import dataclasses
+    rng = np.random.default_rng(seed)
+    D = sv.diag.copy()
+    n = sv.n_nodes
+    for ph in range(2):
+        m = 1.0 + rng.random(n)
+        sub = m * rng.uniform(-spread, spread, n)
+        sup = m * rng.uniform(-spread, spread, n)
+        inner = slice(1, n - 1)  # rows 0 and n-1 stay Dirichlet rows
+        D[ph, 0, inner], D[ph, 1, inner], D[ph, 2, inner] = sub[inner], m[inner], sup[inner]
+        D[ph, 3, inner], D[ph, 5, inner] = alpha * sub[inner], alpha * sup[inner]
+        D[ph, 4, inner] = alpha * m[inner] + rng.uniform(-0.2, 0.2, n)[inner]
+    return dataclasses.replace(sv, diag=D)
+
+
+def _serial_pivots(diag_phase):
+    """The reference's serial sweep (_solve_tridiagonal,
+    discrete_barrier_fdm_pricer_2.py:282-290): pivots beta_i and the
+    contraction |sub_i sup_{i-1}| / beta_i^2 of the c* recurrence."""
+    sub, m, sup = diag_phase[0], diag_phase[1], diag_phase[2]
+    beta = np.empty_like(m)
+    c = 0.0
+    worst = 0.0
+    for i in range(len(m)):
+        beta[i] = m[i] - (sub[i] * c if i else 0.0)
+        if i:
+            worst = max(worst, abs(sub[i] * sup[i - 1]) / beta[i] ** 2)
+        c = sup[i] / beta[i]
+    return beta, worst
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alpha", [-1.0, 1.0], ids=["corrected", "reference_sign"])
+@pytest.mark.parametrize("spread", [0.45, 0.65, 0.75])
+def test_factor_scan_matches_serial_sweep_on_non_dominant_rows(alpha, spread):
+    """fdcn_vc_factor finds the Thomas pivots by a parallel scan
+    over 2x2 matrix products, which equals the reference's serial sweep only
+    to rounding while the recurrence contracts.  Random implicit rows:
+    spread 0.45 all diagonally dominant; 0.65 11 % of rows not dominant,
+    the c* recurrence locally expanding (|sub_i sup_(i-1)| / beta_i^2 up to
+    2.5), pivots >= 0.4; 0.75 23 % not dominant, pivots down to 0.04 (local
+    expansion ~650).  The explicit rows in the reference's sign (alpha = +1)
+    and the corrected one; every scenario of the launch against the serial
+    oracle, in the pointwise form and forced onto the stencil form."""
+    from finite_difference_amd import capi
+    from finite_difference_amd.engine import pack_vc
+    base = _vanilla_solve(1025, 24)
+    solves = [_random_rows(base, seed, alpha, spread) for seed in range(6)]
+    contraction = []
+    for sv in solves:
+        for ph in range(2):
+            beta, worst = _serial_pivots(sv.diag[ph])
+            contraction.append(worst)
+            if spread <= 0.65:
+                assert np.min(np.abs(beta)) > 0.3
+    nondom = np.mean([np.mean(np.abs(sv.diag[1, 0]) + np.abs(sv.diag[1, 2])
+                              > np.abs(sv.diag[1, 1])) for sv in solves])
+    assert (nondom > 0.05 and max(contraction) > 1.0) if spread > 0.6 else nondom < 0.01
+    g = pack_vc(solves, list(range(len(solves))))
+    assert np.all(capi.vc_forms(g.n_nodes, g.n_time, g.n_ranna, g.diag) == 1)
+    ref = oracle_engine().run_vc(solves)
+    w, npt = (lambda p: (p["waves"], p["npt"]))(capi.vc_plan(1025, B=len(solves)))
+    try:
+        for stencil in (False, True):
+            capi.vc_force_variant(w, npt, stencil)
+            got = Engine().run_vc(solves)
+            for k, (a, b) in enumerate(zip(got, ref)):
+                err = float(np.max(np.abs(a - b))) / max(1.0, float(np.max(np.abs(b))))
+                assert err <= 1e-10, (stencil, k, err)
+    finally:
+        capi.vc_force_variant(0, 0, False)

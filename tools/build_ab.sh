@@ -3,7 +3,8 @@
 # tree for "WT") into ab/TAG/libfdcn.so, for A/B timing through bench.py --lib
 # (capi.LIB_PATH).  KREV (optional): take fdcn_kernels.hip alone from that
 # revision, everything else from REV -- a kernel A/B on the current ABI.
-# ABFLAGS (environment): extra hipcc flags, e.g. -DFDCN_STAMPS for a diagnostic build.
+# ABFLAGS (environment): extra hipcc flags, e.g. -DFDCN_STAMPS for a diagnostic build;
+# KSRC: a kernel source file to use in place of fdcn_kernels.hip.
 # Usage: bash tools/build_ab.sh TAG [REV] [KREV]
 set -euo pipefail
 TAG=$1; REV=${2:-WT}; KREV=${3:-}
@@ -18,7 +19,9 @@ else
     git -C "$ROOT" show "$REV:$f" > "$SRC/$f"
   done
 fi
-if [ -n "$KREV" ]; then
+if [ -n "${KSRC:-}" ]; then  # an edited kernel source (diagnostic A/B builds)
+  cp "$KSRC" "$SRC/finite_difference_amd/csrc/fdcn_kernels.hip"
+elif [ -n "$KREV" ]; then
   git -C "$ROOT" show "$KREV:finite_difference_amd/csrc/fdcn_kernels.hip" \
       > "$SRC/finite_difference_amd/csrc/fdcn_kernels.hip"
 fi
