@@ -118,8 +118,8 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed warm-up steps (default: at least 2, continued until "
-                         "WARM_SECONDS of them have run -- the clock ramps over the first "
-                         "~30 ms of work, profiles/r05_small_batch/)")
+                         "WARM_SECONDS of them have run: the clock ramps over the first ~1 s "
+                         "of work, profiles/r05/tail/)")
     ap.add_argument("--workload", choices=sorted(DEFAULT_BATCH) + list(TRADE_WORKLOADS),
                     default="american")
     ap.add_argument("--batch", type=int, default=0, help="scenarios per GPU (0: workload default)")

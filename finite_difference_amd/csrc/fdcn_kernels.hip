@@ -2560,7 +2560,7 @@ const Variant* choose(int n_nodes, int it, int k_cap, long B = 1L << 30) {
   }
   // Batches too small to put a wave on every SIMD, IT march only: the
   // single-trade flavour of the chosen W = 1 variant (in-wave ILP).  Measured
-  // (profiles/r05_small_batch/): trade_american (IT, NPT 32) 8.23 -> 7.47 ms
+  // (profiles/r05/small_batch/): trade_american (IT, NPT 32) 8.23 -> 7.47 ms
   // per trade; but the CN flavour loses everywhere it was timed --
   // trade_cnlog (NPT 8) 0.426 -> 0.496 ms, the config-3 grid (NPT 16) at
   // B = 64 / 256 / 512 / 1024: 0.75 / 0.76 / 0.87 / 0.83 ms -> 0.98 / 0.99 /
