@@ -1114,6 +1114,7 @@ def bench_spot_vc(args):
         "kernel": {"name": f"fdcn_vc_march<{plan['waves']},{plan['npt']}>", **plan,
                    "slots": slots, "slot_use": g.n_nodes / slots},
         "outputs_finite": bool(np.all(np.isfinite(res))), "parity": parity,
+        "out_sha": hashlib.sha256(np.ascontiguousarray(res).tobytes()).hexdigest()[:16],
         "host_build_s": t_build, "cpu_baseline": cpu}), flush=True)
     if parity is not None and not (parity["ok"] and parity["all_finite"]):
         print(f"bench.py: PARITY FAILURE {parity}", file=sys.stderr, flush=True)

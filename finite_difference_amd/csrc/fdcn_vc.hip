@@ -245,17 +245,175 @@ __device__ __forceinline__ double shfl_d(double x, int src) {
   return __shfl(x, src);
 }
 
+// Step 3 of the factor kernel, one phase: the factored rows, 64 consecutive
+// rows at a time (see above).  kFast: the single pass -- the pointwise form
+// at the candidate alpha assumed, the phase classified on the rows as they
+// are factored (count, first and last exceptional row; the first two rows'
+// residuals recorded in xi / xv, since i1 is known only once both phases
+// are); otherwise the form, alpha and i1 are known and the residuals of rows
+// i1 and i1 + 1 go straight to sc.
+struct FactorClass {
+  int cnt, first, last;
+};
+
+template <bool kFast>
+__device__ __forceinline__ FactorClass factor_rows(const double* P, int n, int slots, int pad_lo,
+                                                   int lane, bool pw, double alpha, int i1,
+                                                   double* C, double* sc, int* xi, double* xv) {
+  const double *sub = P, *mn = P + n, *sup = P + 2 * n;
+  const double *ae = P + 3 * n, *be = P + 4 * n, *ce = P + 5 * n;
+  const bool none = i1 < 0;
+  double* cA = C;
+  double* cB = C + slots;
+  double* cC = C + 2 * slots;
+  double* cf = C + 3 * slots;
+  double* cE = C + 4 * slots;
+  for (int s = lane; s < pad_lo; s += 64) {  // lower padding: pass the forward carry up
+    if (!pw) cA[s] = cC[s] = 0.0;
+    cB[s] = 0.0;
+    cf[s] = 1.0;
+    cE[s] = 0.0;
+  }
+  for (int s = pad_lo + n + lane; s < slots; s += 64) {  // upper padding: carry down
+    if (!pw) cA[s] = cC[s] = 0.0;
+    cB[s] = 0.0;
+    cf[s] = 0.0;
+    cE[s] = 1.0;
+  }
+  FactorClass fc{0, 0x7fffffff, -1};
+  M2 carry{1.0, 0.0, 0.0, 1.0};  // the product of every earlier group's matrices
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const bool row = i < n;
+    const double sb = row ? sub[i] : 0.0, m = row ? mn[i] : 1.0, sp = row ? sup[i] : 0.0;
+    M2 T = row ? M2{0.0, sp, -sb, m} : M2{1.0, 0.0, 0.0, 1.0};
+    for (int d = 1; d < 64; d <<= 1) {  // inclusive: rows base..i, later rows on the left
+      const M2 X{shfl_d(T.a, lane - d), shfl_d(T.b, lane - d), shfl_d(T.c, lane - d),
+                 shfl_d(T.d, lane - d)};
+      if (lane >= d) T = mnorm(mmul(T, X));
+    }
+    const M2 Pi = mnorm(mmul(T, carry));  // rows 0..i
+    // c* of row i-1: the previous lane's product, or the carry for lane 0,
+    // applied to (p, q) = (0, 1)
+    double pb = shfl_d(Pi.b, lane - 1), qb = shfl_d(Pi.d, lane - 1);
+    if (lane == 0) {
+      pb = carry.b;
+      qb = carry.d;
+    }
+    carry = M2{shfl_d(Pi.a, 63), shfl_d(Pi.b, 63), shfl_d(Pi.c, 63), shfl_d(Pi.d, 63)};
+    const bool interior = row && i > 0 && i < n - 1;
+    // kFast: this group's exceptional rows (residual not exactly zero)
+    double ra = 0.0, rc = 0.0;
+    bool exc = false;
+    int pre = 2;
+    if constexpr (kFast) {
+      if (interior) {
+        ra = ae[i] - alpha * sb;
+        rc = ce[i] - alpha * sp;
+        exc = ra != 0.0 || rc != 0.0;
+      }
+      const unsigned long long bal = __ballot(exc);
+      if (bal) {
+        if (fc.cnt == 0) fc.first = base + __ffsll((long long)bal) - 1;
+        fc.last = base + 63 - __clzll((long long)bal);
+        pre = fc.cnt + __popcll(bal & ((1ull << lane) - 1ull));
+        fc.cnt += __popcll(bal);
+      }
+    }
+    if (!row) continue;
+    const double cprev = i > 0 ? pb / qb : 0.0;
+    const double beta = (i == 0) ? m : m - sb * cprev;
+    const double g = 1.0 / beta;
+    const double cs = (i < n - 1) ? sp / beta : 0.0;
+    if (i == 0) sc[0] = g;
+    if (i == n - 1) sc[1] = g;
+    if constexpr (kFast) {
+      if (exc && pre < 2) {
+        xi[pre] = i;
+        xv[2 * pre] = g * ra;
+        xv[2 * pre + 1] = g * rc;
+      }
+    } else if (pw && interior && !none && (i == i1 || i == i1 + 1)) {
+      sc[3 + 2 * (i - i1)] = g * (ae[i] - alpha * sb);
+      sc[4 + 2 * (i - i1)] = g * (ce[i] - alpha * sp);
+    }
+    const int s = i + pad_lo;
+    if (s < 0) continue;  // node 0 outside the slots (pad_lo = -1)
+    if (pw) {
+      cB[s] = interior ? g * (be[i] - alpha * m) : 0.0;
+    } else {
+      cA[s] = interior ? ae[i] * g : 0.0;
+      cB[s] = interior ? be[i] * g : 0.0;
+      cC[s] = interior ? ce[i] * g : 0.0;
+    }
+    // node 0 takes the forward carry as its value; node n-1 the backward
+    // one; interior rows their factors
+    cf[s] = (i == 0) ? 1.0 : (i == n - 1 ? 0.0 : -sb * g);
+    cE[s] = (i == n - 1) ? 1.0 : (i == 0 ? 0.0 : -cs);
+  }
+  return fc;
+}
+
+// One workgroup per scenario, one wave per phase.  Round 5: one pass over
+// diag for the common case.  Each wave assumes the pointwise form at the
+// first candidate alpha (the middle row's ratio), factors its rows in that
+// form and classifies them on the way (the rows it reads anyway); if both
+// phases then agree on the pointwise form -- every Pricer2 and analytic-
+// overlay scenario whose middle row is not beside the barrier -- the
+// scenario is done, bitwise what the two-pass path below writes (it would
+// pick the same candidate: the first that classifies).  Otherwise (a phase
+// not classified at that alpha, the stencil form, or the diagnostics'
+// force_stencil) the general path classifies at all three candidates and
+// factors again.  diag read 1.0 times instead of ~1.33 per scenario.
 __global__ void __launch_bounds__(128) fdcn_vc_factor(VcArgs A) {
   __shared__ int agree[2][3];
+  __shared__ int xi[2][2];
+  __shared__ double xv[2][4];
   const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
   const int b = blockIdx.x;
   const int n = A.n, slots = A.slots, pad_lo = A.pad_lo;
   const bool used = ph == 0 ? A.n_ranna > 0 : A.n_ranna < A.n_time;
   const double* P = A.diag + ((size_t)b * 2 + ph) * FDCN_VC_NDIAG * n;
-  const double *sub = P, *mn = P + n, *sup = P + 2 * n;
-  const double *ae = P + 3 * n, *be = P + 4 * n, *ce = P + 5 * n;
+  const double *sub = P, *sup = P + 2 * n;
+  const double *ae = P + 3 * n, *ce = P + 5 * n;
+  double* const scal = A.coef + (size_t)b * ws_scen(A) + 2 * kNC * (size_t)slots;
+  double* const C = A.coef + (size_t)b * ws_scen(A) + (size_t)ph * kNC * slots;
+  double* const sc = scal + 8 * ph;
 
-  // 1. classification: three candidate alphas at once, rows lane-strided
+  if (!A.force_stencil) {
+    const double alpha_c = used ? row_ratio(P, n, n / 2) : 0.0;
+    FactorClass fc{0, 0x7fffffff, -1};
+    if (used)
+      fc = factor_rows<true>(P, n, slots, pad_lo, lane, true, alpha_c, -1, C, sc, xi[ph], xv[ph]);
+    const int okf = fc.cnt <= 2 && (fc.cnt == 0 || fc.last - fc.first <= 1);
+    if (lane == 0) {
+      agree[ph][0] = okf;
+      agree[ph][1] = fc.first;
+      agree[ph][2] = fc.last;
+    }
+    __syncthreads();  // also orders the xi / xv stores before their reads
+    int i1;
+    if (pointwise_form(agree[0][0], agree[0][1], agree[0][2], agree[1][0], agree[1][1],
+                       agree[1][2], &i1)) {
+      if (ph == 0 && lane == 0) {
+        scal[16] = 1.0;
+        scal[17] = (double)i1;
+      }
+      if (used && lane == 0) {
+        sc[2] = alpha_c;
+        sc[3] = sc[4] = sc[5] = sc[6] = 0.0;
+        for (int j = 0; j < fc.cnt && j < 2; ++j) {  // rows i1 / i1 + 1 of this phase
+          sc[3 + 2 * (xi[ph][j] - i1)] = xv[ph][2 * j];
+          sc[4 + 2 * (xi[ph][j] - i1)] = xv[ph][2 * j + 1];
+        }
+      }
+      return;  // uniform: both waves read the same agree[]
+    }
+    __syncthreads();  // agree[] is rewritten below
+  }
+
+  // the general path: 1. classification, three candidate alphas at once,
+  // rows lane-strided
   double al[3] = {0.0, 0.0, 0.0};
   int cnt[3] = {0, 0, 0}, fst[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff}, lst[3] = {-1, -1, -1};
   const bool classify = used && !A.force_stencil;
@@ -303,86 +461,18 @@ __global__ void __launch_bounds__(128) fdcn_vc_factor(VcArgs A) {
   int i1;
   const bool pw = pointwise_form(agree[0][0], agree[0][1], agree[0][2], agree[1][0],
                                  agree[1][1], agree[1][2], &i1);
-  const bool none = i1 < 0;
-  double* C = A.coef + (size_t)b * ws_scen(A);
-  double* scal = C + 2 * kNC * (size_t)slots;
   if (ph == 0 && lane == 0) {
     scal[16] = pw ? 1.0 : 0.0;
     scal[17] = (double)i1;
   }
   if (!used) return;
   const double alpha = pw ? alpha0 : 0.0;
-  C += (size_t)ph * kNC * slots;
-  double* cA = C;
-  double* cB = C + slots;
-  double* cC = C + 2 * slots;
-  double* cf = C + 3 * slots;
-  double* cE = C + 4 * slots;
-  double* sc = scal + 8 * ph;
   if (lane == 0) {
     sc[2] = alpha;
     sc[3] = sc[4] = sc[5] = sc[6] = 0.0;
   }
-  for (int s = lane; s < pad_lo; s += 64) {  // lower padding: pass the forward carry up
-    if (!pw) cA[s] = cC[s] = 0.0;
-    cB[s] = 0.0;
-    cf[s] = 1.0;
-    cE[s] = 0.0;
-  }
-  for (int s = pad_lo + n + lane; s < slots; s += 64) {  // upper padding: carry down
-    if (!pw) cA[s] = cC[s] = 0.0;
-    cB[s] = 0.0;
-    cf[s] = 0.0;
-    cE[s] = 1.0;
-  }
-
-  // 3. the factored rows, 64 consecutive rows at a time
-  M2 carry{1.0, 0.0, 0.0, 1.0};  // the product of every earlier group's matrices
-  for (int base = 0; base < n; base += 64) {
-    const int i = base + lane;
-    const bool row = i < n;
-    const double sb = row ? sub[i] : 0.0, m = row ? mn[i] : 1.0, sp = row ? sup[i] : 0.0;
-    M2 T = row ? M2{0.0, sp, -sb, m} : M2{1.0, 0.0, 0.0, 1.0};
-    for (int d = 1; d < 64; d <<= 1) {  // inclusive: rows base..i, later rows on the left
-      const M2 X{shfl_d(T.a, lane - d), shfl_d(T.b, lane - d), shfl_d(T.c, lane - d),
-                 shfl_d(T.d, lane - d)};
-      if (lane >= d) T = mnorm(mmul(T, X));
-    }
-    const M2 Pi = mnorm(mmul(T, carry));  // rows 0..i
-    // c* of row i-1: the previous lane's product, or the carry for lane 0,
-    // applied to (p, q) = (0, 1)
-    double pb = shfl_d(Pi.b, lane - 1), qb = shfl_d(Pi.d, lane - 1);
-    if (lane == 0) {
-      pb = carry.b;
-      qb = carry.d;
-    }
-    carry = M2{shfl_d(Pi.a, 63), shfl_d(Pi.b, 63), shfl_d(Pi.c, 63), shfl_d(Pi.d, 63)};
-    if (!row) continue;
-    const double cprev = i > 0 ? pb / qb : 0.0;
-    const double beta = (i == 0) ? m : m - sb * cprev;
-    const double g = 1.0 / beta;
-    const double cs = (i < n - 1) ? sp / beta : 0.0;
-    if (i == 0) sc[0] = g;
-    if (i == n - 1) sc[1] = g;
-    const bool interior = i > 0 && i < n - 1;
-    if (pw && interior && !none && (i == i1 || i == i1 + 1)) {
-      sc[3 + 2 * (i - i1)] = g * (ae[i] - alpha * sb);
-      sc[4 + 2 * (i - i1)] = g * (ce[i] - alpha * sp);
-    }
-    const int s = i + pad_lo;
-    if (s < 0) continue;  // node 0 outside the slots (pad_lo = -1)
-    if (pw) {
-      cB[s] = interior ? g * (be[i] - alpha * m) : 0.0;
-    } else {
-      cA[s] = interior ? ae[i] * g : 0.0;
-      cB[s] = interior ? be[i] * g : 0.0;
-      cC[s] = interior ? ce[i] * g : 0.0;
-    }
-    // node 0 takes the forward carry as its value; node n-1 the backward
-    // one; interior rows their factors
-    cf[s] = (i == 0) ? 1.0 : (i == n - 1 ? 0.0 : -sb * g);
-    cE[s] = (i == n - 1) ? 1.0 : (i == 0 ? 0.0 : -cs);
-  }
+  // 3. the factored rows
+  factor_rows<false>(P, n, slots, pad_lo, lane, pw, alpha, i1, C, sc, nullptr, nullptr);
 }
 
 // LDS tables read off a byte address the compiler cannot see through
