@@ -495,9 +495,14 @@ template <int NPT>
 using dvec = double __attribute__((ext_vector_type(NPT)));
 
 // <1, 16> of the stencil form needs 256 VGPRs + 31 AGPRs: held to two waves
-// per SIMD it spills; it runs only the scenarios the pointwise form declines
+// per SIMD it spills; it runs only the scenarios the pointwise form declines.
+// NPT 8 and 10 of the pointwise form are held to three waves per SIMD: NPT 10
+// then spills 124 B a lane, and still runs the reference's default 600 x 600
+// grid faster (1.25 -> 1.17 ms for 4 096 trades, profiles/r05/vc_npt10/)
 template <int W, int NPT, bool PW>
-__global__ void __launch_bounds__(64 * W, (W == 1 && (PW || NPT == 16)) ? 2 : 1)
+__global__ void __launch_bounds__(64 * W, (W == 1 && PW && (NPT == 10 || NPT == 8))
+                                              ? 3
+                                              : ((W == 1 && (PW || NPT == 16)) ? 2 : 1))
     fdcn_vc_march(VcArgs A) {
   __shared__ double xch[6 * W + 2];
   // the twelve lane-scan weights of the phase, [wave][weight][lane]: read
@@ -690,7 +695,11 @@ __global__ void __launch_bounds__(64 * W, (W == 1 && (PW || NPT == 16)) ? 2 : 1)
         // row at slot k of its thread: R[k] += ra V[k-1] + rc V[k+1]; the
         // residuals are zero on every other thread
         auto exc_row = [&](int k, double ra, double rc) __attribute__((always_inline)) {
-          double xm = V[(k + NPT - 1) & (NPT - 1)], xp = V[(k + 1) & (NPT - 1)];
+          // (the neighbour slots wrap; a power-of-two chunk by masking, which
+          // compiles to fewer indexed moves than the selects)
+          constexpr bool kPow2 = (NPT & (NPT - 1)) == 0;
+          double xm = V[kPow2 ? (k + NPT - 1) & (NPT - 1) : (k == 0 ? NPT - 1 : k - 1)];
+          double xp = V[kPow2 ? (k + 1) & (NPT - 1) : (k == NPT - 1 ? 0 : k + 1)];
           if (k == 0) {  // uniform: the slot below is in the thread below
             xm = from_below(xm, 1, lane4);
             if (lo_out && t == 0) xm = v0;
@@ -713,7 +722,8 @@ __global__ void __launch_bounds__(64 * W, (W == 1 && (PW || NPT == 16)) ? 2 : 1)
           R[k] = fma(ra, xm, fma(rc, xp, R[k]));
         };
         exc_row(k1, ra1, rc1);
-        exc_row((k1 + 1) & (NPT - 1), ra2, rc2);
+        exc_row((NPT & (NPT - 1)) == 0 ? (k1 + 1) & (NPT - 1) : (k1 + 1 == NPT ? 0 : k1 + 1), ra2,
+                rc2);
       }
       cw = fma(-alpha, v0, g0 * lo);
       cwb = fma(-alpha, vN, gN * hi);
@@ -883,7 +893,9 @@ VcVariant vmk() {
 }
 // (W = 16 holds at most 128 VGPRs a wave and spills its NPT = 8 and 16
 // bodies; W = 8 NPT = 16 (8 193 nodes) spills less, on half the waves)
-const VcVariant kVc[] = {vmk<1, 4>(),  vmk<1, 8>(),  vmk<1, 16>(), vmk<4, 4>(),
+// (NPT 10 and 12, round 5: the reference's default 600 x 600 grid, 601
+// nodes, fills 640 slots at 94 % instead of 1 024 at 59 %)
+const VcVariant kVc[] = {vmk<1, 4>(),  vmk<1, 8>(),  vmk<1, 10>(), vmk<1, 12>(), vmk<1, 16>(), vmk<4, 4>(),
                          vmk<4, 8>(),  vmk<4, 16>(), vmk<8, 16>(),
                          vmk<16, 4>(), vmk<16, 8>(), vmk<16, 16>()};
 constexpr int kNumVc = sizeof(kVc) / sizeof(kVc[0]);

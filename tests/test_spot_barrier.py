@@ -246,7 +246,8 @@ def _with_exceptional_rows(sv, i1, ko=True):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("w,npt,n", [(1, 16, 1025), (1, 8, 513), (1, 4, 257), (4, 16, 4097),
-                                     (4, 8, 2049), (16, 4, 4096), (1, 16, 1000)])
+                                     (4, 8, 2049), (16, 4, 4096), (1, 16, 1000), (1, 10, 601),
+                                     (1, 10, 641), (1, 12, 769), (1, 12, 700)])
 def test_pointwise_exceptional_rows_at_every_slot_position(w, npt, n):
     """The pointwise form's exceptional rows (csrc/fdcn_vc.hip) at slot 0,
     1, NPT-2 and NPT-1 of a lane, across a lane and a wave boundary, next to
