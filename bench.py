@@ -139,6 +139,12 @@ def parse(argv=None):
     ap.add_argument("--n-time", type=int, default=0, help="0: workload default")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--overlap-streams", action="store_true",
+                    help="also time the same batch launched on two streams in turn (each "
+                         "launch with its own v_out / workspace, consecutive launches "
+                         "overlapping): reported beside the line as overlapped_streams, "
+                         "never its value (DESIGN.md §6, one launch and what concurrency "
+                         "recovers)")
     ap.add_argument("--pcie-launches", type=int, default=2,
                     help="launches timed through the host-array ABI (pcie_inclusive; 0: skip)")
     ap.add_argument("--dry-run", action="store_true",
@@ -618,6 +624,48 @@ def run_rank(args):
                         "march, D2H per launch into one reused v_out buffer; value is the "
                         "HBM-resident rate"}
 
+    # consecutive launches on two streams in turn: a serving loop with two
+    # streams, where one launch's drain overlaps the next one's start
+    overlapped = None
+    if args.overlap_streams and world == 1:
+        # two non-default streams: the default stream would serialise with them
+        sa, sb = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+        outs = (torch.empty_like(V0), torch.empty_like(V0))
+        wss = (torch.empty_like(ws), torch.empty_like(ws))
+
+        def launch(j):
+            if is_it:
+                capi.it_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, P.data_ptr(),
+                                  I.data_ptr(), V0.data_ptr(), F.data_ptr(), outs[j].data_ptr(),
+                                  k_cap, wss[j].data_ptr(), ws_bytes, (sa, sb)[j].cuda_stream)
+            else:
+                capi.cn_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, P.data_ptr(),
+                                  I.data_ptr(), V0.data_ptr(), len(g.mon_step), MS.data_ptr(),
+                                  MR.data_ptr(), outs[j].data_ptr(), k_cap, wss[j].data_ptr(),
+                                  ws_bytes, (sa, sb)[j].cuda_stream)
+        for k in range(4):  # the two streams' first launches out of the timed region
+            launch(k % 2)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(sa)
+        sb.wait_event(e0)
+        for k in range(args.steps):
+            launch(k % 2)
+        j = torch.cuda.Event()
+        j.record(sb)
+        sa.wait_event(j)
+        e1.record(sa)
+        torch.cuda.synchronize()
+        ms2 = e0.elapsed_time(e1) / max(1, args.steps)
+        same = all(bool(np.array_equal(o.cpu().numpy().view(np.int64), res.view(np.int64)))
+                   for o in outs)
+        overlapped = {"ms_per_step": ms2, "node_steps_per_s": node_steps_launch / (ms2 * 1e-3),
+                      "frac": fps * node_steps_launch / (ms2 * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
+                      "steps": args.steps, "outputs_bitwise_equal": same,
+                      "note": "the K launches alternate between two streams, each its own "
+                              "v_out and workspace, timed from the first launch to the last "
+                              "one's end; value is one launch at a time"}
+
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(g, args.cpu_seconds, res)
@@ -683,6 +731,7 @@ def run_rank(args):
             "value_per_gpu": value / world,
             "kernel_ms_per_launch": kernel_ms,
             "pcie_inclusive": pcie,
+            "overlapped_streams": overlapped,
             "kernel": {"name": f"fdcn_march<IT={int(is_it)}>", **plan, "k_cap": k_cap,
                        "src_sha": kernel_src_sha(),
                        "forced": list(fv) if fv[0] else None,
