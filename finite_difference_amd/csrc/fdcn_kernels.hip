@@ -626,6 +626,9 @@ template <int IT, int W, int NPT, int ZG = 0>
 __global__ void __launch_bounds__(64 * W)
 __attribute__((amdgpu_waves_per_eu(kWavesPerEu<IT, W, NPT, ZG>)))
 fdcn_march(KArgs A) {
+#ifdef FDCN_WAVE_TIMES
+  const unsigned long long wave_t0 = __builtin_amdgcn_s_memtime();
+#endif
   constexpr int L = Geo<IT, W, NPT, ZG>::L;
   constexpr int SPB = Geo<IT, W, NPT, ZG>::SPB;
   constexpr bool kPair = Geo<IT, W, NPT, ZG>::kPair;
@@ -2403,6 +2406,23 @@ fdcn_march(KArgs A) {
     }
   }
   // ---- store ---------------------------------------------------------------
+#ifdef FDCN_WAVE_TIMES
+  // diagnostic builds only (tools/wave_times.py): the wave's start and end
+  // clocks and its SIMD, into the scenario's Rannacher save slice
+  if constexpr (kRec) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (lane == 0) {
+      double* wt = A.vsave + (size_t)scen * 64 * NPT;
+      wt[0] = __longlong_as_double((long long)wave_t0);
+      wt[1] = __longlong_as_double((long long)t_end);
+      wt[2] = (double)hw;
+      wt[3] = (double)xcc;
+    }
+  }
+#endif
   double* vout = A.v_out + (size_t)scen * n_nodes;
   const double poison = overflow ? __longlong_as_double(0x7ff8000000000000ll) : 0.0;
   if (active) {
