@@ -66,11 +66,11 @@ def main():
     t1.record(stream)
     torch.cuda.synchronize()
     ms = t0.elapsed_time(t1)
-    # the save slice: after the Dirichlet rows (pad64(n_time) + 32 double2 per
-    # scenario), 64 x NPT doubles per scenario
+    # the save slice is the workspace's last region: 64 x NPT doubles per
+    # scenario after the rows (boundary table, if any, and knock-out masks)
     w = ws.cpu().numpy()
-    bnd_doubles = 2 * (((g.n_time + 63) // 64) * 64 + 32) * g.B
-    vs = w[bnd_doubles:].reshape(g.B, 64 * 64)[:NSCEN]
+    save = 64 * plan["npt"]
+    vs = w[g.B * (plan["ws_bytes_per_scen"] // 8 - save):].reshape(g.B, save)[:NSCEN]
     stamps = vs[:, :NSTEPS * 16].reshape(NSCEN, NSTEPS, 16)[:, :, :8].view(np.int64)
     hw = vs[:, 15].astype(np.int64)
     xcc = vs[:, 14].astype(np.int64)

@@ -57,8 +57,10 @@ def main():
         launch()
         torch.cuda.synchronize()
         w = ws.cpu().numpy()
-        # the save slice follows the knock-out mask rows (32 double2 per scenario)
-        vs = w[2 * 32 * g.B:].reshape(g.B, 64 * 64)
+        # the save slice is the workspace's last region (64 x NPT doubles a
+        # scenario, after the knock-out mask rows)
+        save = 64 * plan["npt"]
+        vs = w[g.B * (plan["ws_bytes_per_scen"] // 8 - save):].reshape(g.B, save)
         t0 = vs[:, 0].view(np.int64).astype(np.float64)
         t1 = vs[:, 1].view(np.int64).astype(np.float64)
         hw = vs[:, 2].astype(np.int64)
