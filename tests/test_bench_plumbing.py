@@ -213,3 +213,30 @@ def test_spot_vc_workload_and_parity_record():
     bad[0, 30] += 1e-6 * max(1.0, np.abs(ref[0]).max())
     _, par = bench.vc_cpu_baseline(g, 0.01, bad)
     assert not par["ok"]
+
+
+def test_warm_up_runs_exactly_w_or_about_a_second(monkeypatch):
+    """bench.warm_up: an explicit --warmup W runs exactly W steps (the
+    contract); without it at least two, then more until WARM_SECONDS of wall
+    time have passed (the clock ramp), syncing every four."""
+    import argparse
+    import time
+    sys.path.insert(0, ROOT)
+    import bench
+    calls, syncs = [], []
+
+    def step():
+        calls.append(1)
+        time.sleep(0.002)
+    assert bench.warm_up(step, argparse.Namespace(warmup=3), lambda: syncs.append(1)) == 3
+    assert len(calls) == 3 and not syncs
+    calls.clear()
+    assert bench.warm_up(step, argparse.Namespace(warmup=0)) == 0 and not calls
+    monkeypatch.setattr(bench, "WARM_SECONDS", 0.05)
+    t0 = time.perf_counter()
+    n = bench.warm_up(step, argparse.Namespace(warmup=None), lambda: syncs.append(1))
+    assert n == len(calls) and n >= 2 and time.perf_counter() - t0 >= 0.05
+    assert len(syncs) == n // 4 + 1  # every fourth step, and once at the end
+    calls.clear()
+    monkeypatch.setattr(bench, "WARM_SECONDS", 0.0)
+    assert bench.warm_up(step, argparse.Namespace(warmup=None)) == 2  # the floor
