@@ -71,11 +71,13 @@ HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec sheet, FP64 vector (FMA = 2 flops)
 VALU_CLOCK_GHZ = 2.4          # peak engine clock: 1024 SIMDs x 1 wave64 fp64 op / 4 clk
 N_SIMD = 1024
-# algorithmic bytes / flops per node-step of the reference
+# algorithmic flops per node-step of the reference
 # algorithm (DESIGN.md §4 derives them from fd_american_equity.py:681-717 and
 # discrete_barrier_fdm_pricer.py:531-546: RHS 5 (+2 for dt*lambda), Thomas
-# with the factorisation hoisted 5, IT update 5)
-BYTES_PER_NODE_STEP = {True: 32, False: 16}   # IT: V and lambda in+out; CN: V in+out
+# with the factorisation hoisted 5, IT update 5).  (§8(d)'s bytes per
+# node-step -- 32 IT, 16 CN, V (and lambda) in and out as if streamed every
+# step -- are not an HBM quantity here: the vector stays in VGPRs; the line
+# reports the measured HBM bytes instead, roofline_records.)
 FLOPS_PER_NODE_STEP = {True: 17, False: 10}
 DEFAULT_BATCH = {"american": 4096, "barrier": 10000, "double": 2048, "analytic": 1 << 20,
                  "spot_vc": 4096}
@@ -279,6 +281,63 @@ def load_counters(workload: str):
     if not rec or rec.get("kernel_src_sha") != kernel_src_sha():
         return None
     return rec
+
+
+def roofline_records(fps: float, node_steps_launch: float, kernel_s: float, ctr) -> dict:
+    """The measurement records of a march line,
+    each against the peak of the resource it measures, so that no achieved
+    figure can exceed its stated peak:
+
+    roofline       the reference algorithm's fp64 flops (fps per node-step:
+                   17 IT, 10 CN) / kernel time, against the fp64 VALU peak --
+                   the binding roof (the value vector never leaves VGPRs);
+    fp64_executed  the fp64 work the hardware actually issued (PMC:
+                   SQ_INSTS_VALU_FMA_F64 x 2 + the other f64 VALU
+                   instructions x 1, x 64 lanes) / kernel time, against the
+                   same peak -- what the fp64 pipe was busy with, whatever the
+                   reference's operation count;
+    hbm            the measured HBM bytes (PMC FETCH_SIZE x 2 + WRITE_SIZE,
+                   profiles/pmc_counters.json) / kernel time, against the
+                   HBM peak (round 5's algorithmic-bytes rate, 32 B per
+                   node-step as if V were streamed every step, reached 12.8x
+                   the HBM peak: it was not an HBM quantity and is gone);
+    valu_issue     SQ_INSTS_VALU per lane node-step and the issue fraction.
+
+    The PMC-derived records are null unless the counters were measured on the
+    current kernel source (load_counters)."""
+    achieved_tf = fps * node_steps_launch / kernel_s / 1e12
+    out = {"roofline": {"bound": "fp64_valu", "achieved": achieved_tf,
+                        "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": achieved_tf / FP64_VALU_PEAK_TFLOPS,
+                        "traffic": ctr.get("hbm_bytes_per_launch") if ctr else None,
+                        "flops_per_node_step": fps},
+           "fp64_executed": None, "hbm": None, "valu_issue": None}
+    if ctr and ctr.get("f64_valu_insts_per_launch") and ctr.get("fma_f64_per_launch") is not None:
+        fma = float(ctr["fma_f64_per_launch"])
+        other = float(ctr["f64_valu_insts_per_launch"]) - fma
+        flops = 64.0 * (2.0 * fma + other)
+        tf = flops / kernel_s / 1e12
+        out["fp64_executed"] = {
+            "flops_per_node_step": flops / node_steps_launch, "achieved": tf,
+            "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_VALU_PEAK_TFLOPS,
+            "note": "PMC of this kernel source: (2 x SQ_INSTS_VALU_FMA_F64 + other f64 VALU "
+                    "instructions) x 64 lanes per launch / kernel time"}
+    if ctr and ctr.get("hbm_bytes_per_launch"):
+        gbs = float(ctr["hbm_bytes_per_launch"]) / kernel_s / 1e9
+        out["hbm"] = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": gbs / HBM_PEAK_GBS,
+                      "bytes_per_launch": float(ctr["hbm_bytes_per_launch"]),
+                      "note": "measured HBM traffic (PMC FETCH_SIZE x 2 + WRITE_SIZE, "
+                              "profiles/pmc_counters.json) / kernel time"}
+    if ctr and ctr.get("valu_insts_per_launch"):
+        insts = float(ctr["valu_insts_per_launch"])
+        out["valu_issue"] = {
+            "valu_insts_per_lane_node_step": 64 * insts / node_steps_launch,
+            "issue_frac": insts * 4 / (N_SIMD * VALU_CLOCK_GHZ * 1e9 * kernel_s),
+            "note": "SQ_INSTS_VALU (wave instructions) of this kernel source "
+                    "(profiles/pmc_counters.json) x 64 lanes / node-steps; issue: x 4 clk "
+                    "per wave64 fp64 op / (1024 SIMDs x 2.4 GHz x launch time)"}
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -499,16 +558,23 @@ def run_rank(args):
             dist.init_process_group("gloo")
         return dry_run_rank(args, world, rank, local)
     from finite_difference_amd import capi, distributed
-    bound = distributed.bind_device()  # this rank's GPU for libfdcn and torch
-    if bound is None:
-        raise capi.FdcnError("no gfx950 device visible; the benchmark needs an MI355X")
+    # this rank's GPU for libfdcn and torch; with several ranks a local
+    # failure is reported through the group's binding check, so every rank
+    # raises together instead of the others waiting for it in a collective
+    bound = distributed.bind_device(raise_local=world == 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.backend == "nccl":
+        if args.backend == "nccl" and bound is not None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", bound))
+        elif args.backend == "nccl":
+            dist.init_process_group("nccl")
         else:
             dist.init_process_group("gloo")
-        distributed.check_device_binding(bound)  # no two ranks on one GPU unless shared
+        err = distributed.bind_error() or (
+            None if bound is not None else "no gfx950 device visible to this rank")
+        distributed.check_device_binding(bound, err)  # no two ranks on one GPU unless shared
+    if bound is None:
+        raise capi.FdcnError("no gfx950 device visible; the benchmark needs an MI355X")
     if args.force_variant:
         capi.force_variant(*[int(x) for x in args.force_variant.split(",")])
     dev = torch.device("cuda", bound)
@@ -591,11 +657,10 @@ def run_rank(args):
     value = total / elapsed
     workload = (f"{label}_{n_space}x{n_time}_total{args.total}" if args.total
                 else f"{label}_{n_space}x{n_time}_batch{B}")
-    bps, fps = BYTES_PER_NODE_STEP[is_it], FLOPS_PER_NODE_STEP[is_it]
+    fps = FLOPS_PER_NODE_STEP[is_it]
     kernel_s = kernel_ms * 1e-3
-    achieved_tf = fps * node_steps_launch / kernel_s / 1e12
-    achieved_gbs = bps * node_steps_launch / kernel_s / 1e9
     ctr = load_counters(workload)
+    recs = roofline_records(fps, node_steps_launch, kernel_s, ctr)
 
     # the PCIe-inclusive rate of the host-array boundary (fdcn_it_batch /
     # fdcn_cn_batch with NumPy arrays: H2D of the plan, the march, D2H of
@@ -689,14 +754,6 @@ def run_rank(args):
         else:
             config.update(option="double knock-out call", monitoring="every step",
                           rannacher_steps=2)
-        valu = None
-        if ctr and ctr.get("valu_insts_per_launch"):
-            insts = float(ctr["valu_insts_per_launch"])
-            valu = {"valu_insts_per_lane_node_step": 64 * insts / node_steps_launch,
-                    "issue_frac": insts * 4 / (N_SIMD * VALU_CLOCK_GHZ * 1e9 * kernel_s),
-                    "note": "SQ_INSTS_VALU (wave instructions) of this kernel source "
-                            "(profiles/pmc_counters.json) x 64 lanes / node-steps; issue: x 4 clk "
-                            "per wave64 fp64 op / (1024 SIMDs x 2.4 GHz x launch time)"}
         fv = capi.forced_variant()
         line = {
             "metric": "CN grid-node-steps/sec/GPU (2048x4096 grid); achieved HBM GB/s vs peak",
@@ -716,18 +773,9 @@ def run_rank(args):
                 args.workload] + ")",
             "config": config,
             # the binding roof: the march keeps V in VGPRs, so HBM never binds
-            # (DESIGN.md §4); fp64 FMA throughput does
-            "roofline": {"bound": "fp64_valu", "achieved": achieved_tf,
-                         "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / FP64_VALU_PEAK_TFLOPS,
-                         "traffic": ctr.get("hbm_bytes_per_launch") if ctr else None,
-                         "flops_per_node_step": fps},
-            "roofline_hbm_effective": {
-                "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "bytes_per_node_step": bps,
-                "note": "algorithmic bytes (SURVEY 8d) / kernel time: an effective rate; the "
-                        "measured HBM traffic is roofline.traffic bytes per launch"},
-            "valu_issue": valu,
+            # (DESIGN.md §4); fp64 FMA throughput does -- beside it the fp64
+            # work actually executed and the measured HBM rate (roofline_records)
+            **recs,
             "value_per_gpu": value / world,
             "kernel_ms_per_launch": kernel_ms,
             "pcie_inclusive": pcie,
@@ -765,10 +813,14 @@ def dry_run_rank(args, world: int, rank: int, local: int):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ranks = [{"rank": rank, "local_rank": local, "pid": os.getpid()}]
-    if args.total:  # the shard this rank would march (config 4)
+    if args.total:  # the shard this rank would march (config 4), built
         from finite_difference_amd.distributed import shard_range
         r = shard_range(args.total, rank, world)
         ranks[0]["shard"] = [r.start, r.stop]
+        builder, ns0, nt0, _, _ = WORKLOADS[args.workload]
+        g = builder(args.total, args.n_space or ns0, args.n_time or nt0, seed=0, select=r)
+        ranks[0]["batch"] = int(g.B)
+        ranks[0]["params_sha"] = hashlib.sha256(g.params.tobytes()).hexdigest()[:16]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1125,7 +1177,6 @@ def bench_spot_vc(args):
     node_steps = g.B * units * g.n_time
     fps = FLOPS_PER_NODE_STEP[False]
     tf = fps * node_steps / (kernel_ms * 1e-3) / 1e12
-    gbs = BYTES_PER_NODE_STEP[False] * node_steps / (kernel_ms * 1e-3) / 1e9
     slots = 64 * plan["waves"] * plan["npt"]
     # PMC of this workload (profiles/pmc_counters.json), only if measured on
     # the current fdcn_vc.hip
@@ -1157,8 +1208,15 @@ def bench_spot_vc(args):
                         "march_issue_frac": ctr["march"]["valu_issue_utilisation"],
                         "note": "profiles/pmc_counters.json, measured on this fdcn_vc.hip"}
                        if ctr else None),
-        "roofline_hbm_effective": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "bytes_per_node_step": BYTES_PER_NODE_STEP[False]},
+        # measured HBM bytes of both kernels per launch / launch time (PMC)
+        "hbm": ({"achieved": (ctr["march"]["hbm_bytes_per_launch"]
+                              + ctr["factor"]["hbm_bytes_per_launch"]) / (kernel_ms * 1e-3) / 1e9,
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": (ctr["march"]["hbm_bytes_per_launch"]
+                          + ctr["factor"]["hbm_bytes_per_launch"]) / (kernel_ms * 1e-3) / 1e9
+                         / HBM_PEAK_GBS,
+                 "note": "PMC FETCH_SIZE x 2 + WRITE_SIZE of the march and factor kernels"}
+                if ctr else None),
         "kernel_ms_per_launch": kernel_ms,
         "kernel": {"name": f"fdcn_vc_march<{plan['waves']},{plan['npt']}>", **plan,
                    "slots": slots, "slot_use": g.n_nodes / slots},

@@ -54,6 +54,7 @@
 #include "../../include/fdcn.h"
 #include "../../include/fdcn_diag.h"
 #include "fdcn_shared.h"
+#include "fdcn_ko_res.h"
 
 namespace {
 
@@ -368,6 +369,12 @@ struct MonRun {
 // exec-masked v_mov_b64 per slot.  (NPT = 16 joined in round 2: config 3,
 // daily monitoring, 4 VALU per wave and step fewer on average.)
 constexpr int kKoRow = 32;
+// The recovery-form variants' row continues with the resident projection's
+// run masks and group codes (kKoRes; fdcn_ko_res.h): q0, q1, q2, qd, then the
+// two code words -- loaded by the projection itself (kept live through the
+// march they pushed the kernel's SGPRs into VGPR lanes: 260 registers, one
+// wave per SIMD)
+constexpr int kKoResRow = 4;
 typedef unsigned KoMask8 __attribute__((ext_vector_type(8)));  // 4 masks, s_load_dwordx8
 __device__ __forceinline__ unsigned long long ko_pair8(KoMask8 m, int j) {
   return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];
@@ -601,7 +608,8 @@ __host__ __device__ inline int lds_doubles_per_scen(int lz) {
   return ((ZG & 1) ? 0 : sm_doubles(IT, W, NPT, ZG, lz)) +
          (Geo<IT, W, NPT, ZG>::kPhiLds ? 64 * W * NPT : 0) +
          (W > 1 ? Xch<W>::kSize : 0) + (Geo<IT, W, NPT, ZG>::kScanLds ? kScanLdsDoubles : 0) +
-         (Geo<IT, W, NPT, ZG>::kBndLds ? 128 * W : 0);
+         (Geo<IT, W, NPT, ZG>::kBndLds ? 128 * W : 0) +
+         (rec_form(IT, W, NPT) ? 2 : 0);  // the knock-out rebate slot (fdcn_ko_res.h)
 }
 
 // Issue priority of the zero-carry passes and the carry scans.  Each sweep
@@ -622,9 +630,17 @@ __host__ __device__ inline int lds_doubles_per_scen(int lz) {
 template <int IT, int W, int NPT, int ZG>
 constexpr int kWavesPerEu = (!IT && W == 1 && NPT == 16 && !(ZG & 6)) ? 4 : 1;
 
+// The register target the compiler is held to: the recovery-form variants
+// (config 5) are held to two waves per SIMD (256 registers), where they sit
+// at the edge: unconstrained, the resident-mask projection's build put 4 values
+// of the boundary evaluation into AGPRs (260 registers, one wave per SIMD);
+// held, they spill to scratch in the once-per-64-steps evaluation instead.
+template <int IT, int W, int NPT, int ZG>
+constexpr int kWavesTarget = rec_form(IT, W, NPT) ? 2 : kWavesPerEu<IT, W, NPT, ZG>;
+
 template <int IT, int W, int NPT, int ZG = 0>
 __global__ void __launch_bounds__(64 * W)
-__attribute__((amdgpu_waves_per_eu(kWavesPerEu<IT, W, NPT, ZG>)))
+__attribute__((amdgpu_waves_per_eu(kWavesTarget<IT, W, NPT, ZG>)))
 fdcn_march(KArgs A) {
 #ifdef FDCN_WAVE_TIMES
   const unsigned long long wave_t0 = __builtin_amdgcn_s_memtime();
@@ -682,6 +698,10 @@ fdcn_march(KArgs A) {
                       xch + (W > 1 ? Xch<W>::kSize : 0) + (kScanLds ? kScanLdsDoubles : 0)) +
                   (kBndLds ? wave * 64 : 0);
   (void)bblk;
+  // the rebate the resident-mask projection reads back into the knocked-out
+  // slots (rec_form variants: ds_read_b64, fdcn_ko_res.h)
+  double* ko_rbs = reinterpret_cast<double*>(bblk + (kBndLds ? 64 * W : 0));
+  (void)ko_rbs;
 
   const double* P = A.params + (size_t)scen * FDCN_NPARAM;
   const int32_t* I = A.iparams + (size_t)scen * FDCN_NIPARAM;
@@ -722,7 +742,7 @@ fdcn_march(KArgs A) {
   constexpr bool kTabSplit = tab_form(IT, W, NPT, (ZG >> 1) & 1);
   double2* bnd = reinterpret_cast<double2*>(A.bnd) +
                  ((size_t)scen * W + wave) *
-                     (kKoRow + (kGen ? 0 : A.n_pad * (kTabSplit ? 2 : 1)));
+                     (kKoRow + (kGen ? kKoResRow : A.n_pad * (kTabSplit ? 2 : 1)));
   double2* kom_row = bnd + (kGen ? 0 : A.n_pad);
   double2* bnd_raw = kom_row + kKoRow;  // kTabSplit only
   (void)bnd_raw;
@@ -1671,6 +1691,9 @@ fdcn_march(KArgs A) {
   const unsigned long long shrt_ballot = kSplit ? (unsigned long long)__ballot(shrt) : 0ull;
   (void)shrt_ballot;
   unsigned long long kom_addr = 0;  // this wave's mask row (KoLoad variants)
+  // kKoRes: the resident-mask projection (fdcn_ko_res.h), its run masks and
+  // group codes after the mask row (kKoResRow)
+  constexpr bool kKoRes = kRec && !(ZG & 6);
   unsigned long long kom_addr2 = 0, kom_addr12 = 0;  // kPair: second scenario's / both
   if constexpr (KoLoad<IT, W, NPT, ZG>::value) {
     unsigned long long* kom = reinterpret_cast<unsigned long long*>(kom_row);
@@ -1707,6 +1730,57 @@ fdcn_march(KArgs A) {
       kom_addr12 = kom_addr + 32 * sizeof(unsigned long long);
     } else {
       kom_addr = ka;
+    }
+    if constexpr (kKoRes) {
+      // the run masks and per-group codes of the resident projection
+      // (ko_groups): change points are the slots k in [1, NPT-2] whose mask
+      // differs from slot k-1's
+      const unsigned long long mk = lane < NPT ? slot_mask(kml, kmh, lane) : 0ull;
+      const unsigned long long mkp =
+          ((unsigned long long)(unsigned)__shfl_up((int)(mk >> 32), 1, 64) << 32) |
+          (unsigned)__shfl_up((int)(unsigned)mk, 1, 64);
+      const unsigned long long chg =
+          (unsigned long long)__ballot(lane >= 1 && lane < NPT - 1 && mk != mkp);
+      auto rl64 = [](unsigned long long x, int l) {
+        return ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
+               (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, l);
+      };
+      const int nchg = __builtin_popcountll(chg);
+      const int c1 = nchg >= 1 ? uni_i(__builtin_ctzll(chg)) : 0;
+      const int c2 = nchg >= 2 ? uni_i(__builtin_ctzll(chg & (chg - 1))) : 0;
+      const unsigned long long q0 = rl64(mk, 0);
+      const unsigned long long q1 = nchg >= 1 ? rl64(mk, c1) : q0;
+      const unsigned long long q2 = nchg >= 2 ? rl64(mk, c2) : q1;
+      const unsigned long long qd = rl64(mk, NPT - 1);
+      unsigned codes0 = 0u, codes1 = 0u;
+#pragma unroll
+      for (int g = 0; g < NPT / 8; ++g) {
+        const int lo = 8 * g, gsz = (g + 1 == NPT / 8) ? 7 : 8;
+        const unsigned long long bits = (chg >> lo) & ((1ull << gsz) - 1ull);
+        unsigned code;
+        if (nchg > 2) {
+          code = 63u;
+        } else if (bits == 0ull) {
+          code = 0u;
+        } else if ((bits & (bits - 1ull)) == 0ull) {
+          code = 1u + (unsigned)__builtin_ctzll(bits);
+        } else {
+          const int o1 = __builtin_ctzll(bits), o2 = __builtin_ctzll(bits & (bits - 1ull));
+          code = (unsigned)(gsz + 1 + o1 * (2 * gsz - o1 - 1) / 2 + (o2 - o1 - 1));
+        }
+        if (g < 5) codes0 |= code << (6 * g);
+        else codes1 |= code << (6 * (g - 5));
+      }
+      // after the 64 slot masks (kKoResRow): vector stores by lane 0, drained
+      // with the row's below
+      if (lane == 0) {
+        kom[2 * kKoRow + 0] = q0;
+        kom[2 * kKoRow + 1] = q1;
+        kom[2 * kKoRow + 2] = q2;
+        kom[2 * kKoRow + 3] = qd;
+        kom[2 * kKoRow + 4] = ((unsigned long long)codes1 << 32) | codes0;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
   (void)kom_addr2;
@@ -2302,7 +2376,11 @@ fdcn_march(KArgs A) {
     const bool hit1 = !IT && m + 1 == mon.next;
     const bool hit2 = kPair && m + 1 == mon2.next;  // a paired wave's second scenario
     FDCN_STAMP(5);
+#if defined(FDCN_DIAG_KO) && FDCN_DIAG_KO == 3  // diagnostic: no knock-out at all
+    if (false && (hit1 || hit2)) {
+#else
     if (hit1 || hit2) {  // knock-out projection (uniform branch)
+#endif
       const double reb = kPair ? (half ? mon2.cur : mon.cur) : mon.cur;
       double rebv = reb;  // VGPR copy: v_cndmask takes the mask as its SGPR operand
       asm volatile("" : "+v"(rebv));
@@ -2313,7 +2391,60 @@ fdcn_march(KArgs A) {
       // exec-masked v_mov_b64 per slot (config 5: 29.3 -> 26.0 ms per
       // launch).  Rebuilding the masks on the scalar unit from (full, part,
       // k0, k1) measured slower still (34.8 ms): five SALU per slot.
-      if constexpr (KoLoad<IT, W, NPT, ZG>::value) {
+      if constexpr (kKoRes) {
+        // run masks and group codes by six scalar loads off the row (one
+        // wait), then the slots group by group (fdcn_ko_res.h)
+        const unsigned long long sv = __builtin_amdgcn_read_exec();
+        unsigned long long q0, q1, q2, qd, mt;
+        unsigned c0, c1, cd;
+#if defined(FDCN_DIAG_KO) && FDCN_DIAG_KO == 1  // diagnostic: no loads (wrong masks)
+        asm volatile("s_mov_b64 %0, 0\n\ts_mov_b64 %1, 0\n\ts_mov_b64 %2, 0\n\ts_mov_b64 %3, 0\n\t"
+                     "s_mov_b32 %4, 0\n\ts_mov_b32 %5, 0"
+                     : "=s"(q0), "=s"(q1), "=s"(q2), "=s"(qd), "=s"(c0), "=s"(c1));
+#else
+        asm volatile("s_load_dwordx2 %0, %6, %7\n\ts_load_dwordx2 %1, %6, %8\n\t"
+                     "s_load_dwordx2 %2, %6, %9\n\ts_load_dwordx2 %3, %6, %10\n\t"
+                     "s_load_dword %4, %6, %11\n\ts_load_dword %5, %6, %12\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=s"(q0), "=s"(q1), "=s"(q2), "=s"(qd), "=s"(c0), "=s"(c1)
+                     : "s"(kom_addr), "i"(16 * kKoRow), "i"(16 * kKoRow + 8),
+                       "i"(16 * kKoRow + 16), "i"(16 * kKoRow + 24), "i"(16 * kKoRow + 32),
+                       "i"(16 * kKoRow + 36)
+                     : "memory");
+#endif
+        // two statements of 32 slots (the front end counts a tied operand
+        // twice against the register file); exec is restored between them
+        // (the rebate moves in through the LDS unit, ds_read_b64, not the
+        // VALU: FDCN_KO_VMOV builds the v_mov_b64 form for A/B)
+        const unsigned la = lds_addr(ko_rbs);
+#ifdef FDCN_KO_VMOV
+#define FDCN_KO_RES_FORM(N, B) FDCN_KO_RES_ASM_##N##_##B
+#else
+#define FDCN_KO_RES_FORM(N, B) FDCN_KO_RESL_ASM_##N##_##B
+#endif
+#define FDCN_KO_RES_CALL(N, B)                                                             \
+  asm volatile(FDCN_KO_RES_FORM(N, B)                                                      \
+               : FDCN_KO_RES_VOPS_##N##_##B, [q0] "+s"(q0), [q1] "+s"(q1), [cd] "=&s"(cd), \
+                 [mt] "=&s"(mt)                                                           \
+               : FDCN_KO_RES_INS(rebv, sv, q2, qd, c0, c1, kom_addr, la)                  \
+               : "scc", "memory")
+#if defined(FDCN_DIAG_KO) && FDCN_DIAG_KO == 2  // diagnostic: the loads only
+        asm volatile("" ::"s"(q0), "s"(q1), "s"(q2), "s"(qd), "s"(c0), "s"(c1), "v"(rebv));
+        (void)mt;
+        (void)cd;
+        (void)sv;
+#else
+        if constexpr (NPT == 64) {
+          FDCN_KO_RES_CALL(64, 0);
+          FDCN_KO_RES_CALL(64, 1);
+        } else {
+          FDCN_KO_RES_CALL(48, 0);
+          FDCN_KO_RES_CALL(48, 1);
+        }
+#endif
+#undef FDCN_KO_RES_CALL
+#undef FDCN_KO_RES_FORM
+      } else if constexpr (KoLoad<IT, W, NPT, ZG>::value) {
         // eight slots per block: each slot is one v_mov_b64 of the rebate
         // under an exec mask set on the scalar unit (s_and_b64 with the
         // saved exec), while the next block's eight masks arrive (one
@@ -2632,7 +2763,8 @@ int pad64(int n) { return ((n > 0 ? n : 1) + 63) / 64 * 64; }
 // Rannacher save slice [64][NPT]
 size_t bnd_bytes_per_scen(const Variant& v, int n_time) {
   const size_t table = rec_form(v.it, v.w, v.npt)
-                           ? 0 : (size_t)pad64(n_time) * (tab_form(v.it, v.w, v.npt, v.lat) ? 2 : 1);
+                           ? kKoResRow
+                           : (size_t)pad64(n_time) * (tab_form(v.it, v.w, v.npt, v.lat) ? 2 : 1);
   return sizeof(double) * 2 * (table + kKoRow) * (size_t)v.w;
 }
 size_t zg_bytes_per_scen(const Variant& v, int lz) {

@@ -56,71 +56,108 @@ def _single_device_for_every_rank() -> bool:
     return int(os.environ.get("LOCAL_WORLD_SIZE", "1")) <= 1
 
 
-def bind_device() -> Optional[int]:
+def _choose_device(ords) -> int:
+    """The HIP ordinal local rank LOCAL_RANK binds among the visible gfx950
+    ordinals (bind_device), or FdcnError."""
+    from . import capi
+    lr = local_rank()
+    if lr < len(ords) and (len(ords) > 1 or lr == 0):
+        return ords[lr]
+    if len(ords) == 1 and _single_device_for_every_rank():
+        return ords[0]
+    raise capi.FdcnError(
+        f"LOCAL_RANK={lr} (LOCAL_WORLD_SIZE={os.environ.get('LOCAL_WORLD_SIZE', '?')}) but "
+        f"only {len(ords)} gfx950 device(s) are visible; give each rank its own device "
+        f"(HIP_VISIBLE_DEVICES) or set FDCN_SHARE_DEVICE=1 to share one on purpose")
+
+
+def bind_device(raise_local: bool = True) -> Optional[int]:
     """One process per GPU: make this rank's GPU current for libfdcn (the
     host-array entry points run on the calling thread's HIP device) and for
     torch (RCCL collectives need it).  Local rank k binds the k-th visible
     gfx950 device (its HIP ordinal may differ on a host with other GPUs).
     When exactly one device is visible every rank binds it only if the
     launcher gave each rank its own (see _single_device_for_every_rank);
-    otherwise local ranks > 0 raise, as they do when several devices are
+    otherwise local ranks > 0 fail, as they do when several devices are
     visible but fewer than the local rank needs: every rank silently marching
     on GPU 0 is the failure this guards.  Returns the HIP ordinal, or None on
-    a host with no gfx950 device (CPU tests over gloo)."""
+    a host with no gfx950 device (CPU tests over gloo).
+
+    Once the process group exists, every rank enters the binding check
+    (check_device_binding) whatever happened locally -- a rank with no
+    device or a failed binding reports it there -- so every rank raises
+    together and none is left waiting in the collective.  Before
+    the group exists a failure raises at once; a caller that forms the group
+    afterwards (bench.py) passes raise_local=False, keeps the error from
+    bind_error() and hands it to check_device_binding after forming it."""
     from . import capi
+    global _bind_error
+    _bind_error = None
+    dev = None
     try:
         ords = capi.device_ordinals()
     except capi.FdcnError:
-        return None
-    if not ords:
-        return None
-    lr = local_rank()
-    if lr < len(ords) and (len(ords) > 1 or lr == 0):
-        dev = ords[lr]
-    elif len(ords) == 1 and _single_device_for_every_rank():
-        dev = ords[0]
-    else:
-        raise capi.FdcnError(
-            f"LOCAL_RANK={lr} (LOCAL_WORLD_SIZE={os.environ.get('LOCAL_WORLD_SIZE', '?')}) but "
-            f"only {len(ords)} gfx950 device(s) are visible; give each rank its own device "
-            f"(HIP_VISIBLE_DEVICES) or set FDCN_SHARE_DEVICE=1 to share one on purpose")
-    capi.select_device(dev)
+        ords = []
     try:
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.set_device(dev)
-    except ImportError:  # pragma: no cover - torch is always present here
-        pass
+        if ords:
+            dev = _choose_device(ords)
+            capi.select_device(dev)
+            try:
+                import torch
+                if torch.cuda.is_available():
+                    torch.cuda.set_device(dev)
+            except ImportError:  # pragma: no cover - torch is always present here
+                pass
+    except capi.FdcnError as e:
+        _bind_error, dev = str(e), None
     if is_initialized():  # bound after the group formed (the scenario runners)
-        check_device_binding(dev)
+        check_device_binding(dev, _bind_error)
+    elif _bind_error and raise_local:
+        raise capi.FdcnError(_bind_error)
     return dev
+
+
+_bind_error: Optional[str] = None
+
+
+def bind_error() -> Optional[str]:
+    """The local failure of the last bind_device(raise_local=False), if any."""
+    return _bind_error
 
 
 _VISIBLE_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
 
 
-def check_device_binding(dev: Optional[int]) -> None:
-    """Collective check, once the group exists, that no two ranks of a host
-    march on the same GPU unless they were told to share it.  bind_device
-    accepts a non-empty *_VISIBLE_DEVICES with one visible device as a
-    per-rank assignment, which a job-wide HIP_VISIBLE_DEVICES=0 with several
-    local ranks also looks like.  Every rank reports (host name,
-    its visible-device variables, the HIP ordinal it bound): two equal
-    reports name the same physical device.  The decision is taken on the
-    gathered list, so every rank raises together (none is left waiting in a
-    later collective)."""
+def check_device_binding(dev: Optional[int], local_error: Optional[str] = None) -> None:
+    """Collective check, once the group exists, that every rank bound a
+    device and that no two ranks of a host march on the same GPU unless they
+    were told to share it.  bind_device accepts a non-empty *_VISIBLE_DEVICES
+    with one visible device as a per-rank assignment, which a job-wide
+    HIP_VISIBLE_DEVICES=0 with several local ranks also looks like (ADVICE
+    r4).  Every rank reports (host name, its visible-device variables, the
+    HIP ordinal it bound) and its local binding error, if any: a rank-local
+    failure becomes every rank's error, and two equal reports name the same
+    physical device.  The decision is taken on the gathered list, so every
+    rank raises together (none is left waiting in a later collective)."""
     import socket
     from . import capi
     d = _dist()
     if d is None:
+        if local_error:
+            raise capi.FdcnError(local_error)
         return
     share = os.environ.get("FDCN_SHARE_DEVICE") == "1"
     me = None if dev is None else (socket.gethostname(),
                                    tuple(os.environ.get(v, "") for v in _VISIBLE_VARS), int(dev))
     reports = [None] * d.get_world_size()
-    d.all_gather_object(reports, (me, share))
+    d.all_gather_object(reports, (me, share, local_error))
+    failed = [(r, rep[2]) for r, rep in enumerate(reports) if len(rep) > 2 and rep[2]]
+    if failed:
+        raise capi.FdcnError("device binding failed on rank(s) " +
+                             "; ".join(f"{r}: {msg}" for r, msg in failed))
     seen = {}
-    for r, (key, sh) in enumerate(reports):
+    for r, rep in enumerate(reports):
+        key, sh = rep[0], rep[1]
         if key is None:
             continue
         if key in seen and not (sh and reports[seen[key]][1]):

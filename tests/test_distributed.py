@@ -207,3 +207,69 @@ def test_gather_columns_without_a_group_is_identity():
     import numpy as np
     cols = {"a": [1, 2], "b": np.arange(2.0)}
     assert fdist.gather_columns(cols) is cols
+
+
+def test_bind_device_eight_gfx950_ordinals(monkeypatch):
+    """An 8-GPU node: local rank k binds the k-th of eight
+    stubbed gfx950 ordinals, and the group's binding check passes the eight
+    distinct reports."""
+    import socket
+    from finite_difference_amd import capi
+    host = socket.gethostname()
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+              "FDCN_SHARE_DEVICE"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    chosen = []
+    monkeypatch.setattr(capi, "select_device", lambda d: chosen.append(d))
+    monkeypatch.setattr(capi, "device_ordinals", lambda: list(range(8)))
+    reports = {r: ((host, ("", "", ""), r), False, None) for r in range(8)}
+    for k in range(8):
+        monkeypatch.setenv("LOCAL_RANK", str(k))
+        fake = _FakeDist(k, 8, reports)
+        monkeypatch.setattr(fdist, "_dist", lambda: fake)
+        assert fdist.bind_device() == k and chosen[-1] == k
+
+
+def test_bind_device_failure_reaches_every_rank(monkeypatch):
+    """once the group exists a rank whose binding fails still
+    enters the collective check with its error, and every rank raises
+    together -- none waits in all_gather_object for it."""
+    import socket
+    from finite_difference_amd import capi
+    host = socket.gethostname()
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+              "FDCN_SHARE_DEVICE"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    monkeypatch.setattr(capi, "select_device", lambda d: None)
+    monkeypatch.setattr(capi, "device_ordinals", lambda: [0])
+    err = "LOCAL_RANK=1 ... only 1 gfx950 device(s) are visible"
+    # rank 1 fails locally (two local ranks, one visible device): it raises,
+    # and only after contributing its report to the collective
+    calls = []
+
+    class Spy(_FakeDist):
+        def all_gather_object(self, out, obj):
+            calls.append(obj)
+            super().all_gather_object(out, obj)
+    fake = Spy(1, 2, {0: ((host, ("", "", ""), 0), False, None)})
+    monkeypatch.setattr(fdist, "_dist", lambda: fake)
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    with pytest.raises(capi.FdcnError, match="rank"):
+        fdist.bind_device()
+    assert len(calls) == 1 and calls[0][0] is None and calls[0][2]
+    # rank 0 bound its device fine, but raises with rank 1's error
+    fake = _FakeDist(0, 2, {1: (None, False, err)})
+    monkeypatch.setattr(fdist, "_dist", lambda: fake)
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    with pytest.raises(capi.FdcnError, match="rank\\(s\\) 1"):
+        fdist.bind_device()
+    # before the group exists: raise at once, or hand the error back
+    monkeypatch.setattr(fdist, "_dist", lambda: None)
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    with pytest.raises(capi.FdcnError):
+        fdist.bind_device()
+    assert fdist.bind_device(raise_local=False) is None and "LOCAL_RANK=1" in fdist.bind_error()
+    with pytest.raises(capi.FdcnError):
+        fdist.check_device_binding(None, fdist.bind_error())
