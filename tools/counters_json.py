@@ -62,12 +62,47 @@ def expected(wl):
     rd = g.params.nbytes + g.iparams.nbytes + vec * (2 if is_it else 1)
     rd += len(g.mon_step) * 12
     bnd = g.B * waves * n_pad * 16
+    raw_wr = 0
+    if not is_it and waves == 1 and plan["npt"] <= 40:
+        # the one-scenario split form (round 6): one-sided tables and the raw
+        # values of the steps read after an edge knock-out (fdcn_kernels.hip kTab1)
+        bnd, raw_wr = one_sided_table_bytes(g, n_pad)
     ko_row = g.B * waves * plan["npt"] * 8 if (not is_it and plan["npt"] >= 48) else 0
     rec = (g.B * 64 * plan["npt"] * 8 * min(g.n_ranna, g.n_time)
            if (not is_it and waves == 1 and plan["npt"] > 40) else 0)
     key = f"{label}_{ns}x{nt}_batch{B}"
     node_steps = g.B * bench.node_units(g) * g.n_time
-    return key, rd + bnd + ko_row + rec, vec + bnd + ko_row + rec, plan, node_steps
+    return key, rd + bnd + ko_row + rec, vec + bnd + raw_wr + ko_row + rec, plan, node_steps
+
+
+def one_sided_table_bytes(g, n_pad):
+    """(table bytes written = read, raw-value bytes written) of the kTab1
+    variants: a scenario whose lower / upper Dirichlet side has zero
+    coefficients keeps the other side alone (8 B a step); the raw values are
+    stored for the steps after the monitor dates of a scenario whose
+    knock-out reaches an edge node, and for the last step."""
+    import math
+    from finite_difference_amd import capi
+    P, I = g.params, g.iparams
+    table = raw = 0
+    for b in range(g.B):
+        t_a, t_b = P[b, capi.P_TAU0], P[b, capi.P_TAU0] + 1.01 * g.n_time * P[b, capi.P_DT]
+
+        def const(form, c0, e0, c1, e1):
+            zero = (c0 == 0 or c1 == 0) if form == 1 else (c0 == 0 and c1 == 0)
+            return (zero and math.isfinite(c0) and math.isfinite(c1) and
+                    max(e0 * t_a, e0 * t_b, e1 * t_a, e1 * t_b) <= 700.0)
+        lo = const(I[b, capi.I_LO_FORM], *P[b, capi.P_LO_C0:capi.P_LO_E1 + 1])
+        hi = const(I[b, capi.I_HI_FORM], *P[b, capi.P_HI_C0:capi.P_HI_E1 + 1])
+        w = 8 if (lo or hi) else 16
+        table += n_pad * w
+        edge = I[b, capi.I_KO_LO] >= 0 or g.n_nodes - 1 >= I[b, capi.I_KO_HI]
+        ms, mc = I[b, capi.I_MON_START], I[b, capi.I_MON_COUNT]
+        need = {g.n_time - 1}
+        if edge:
+            need |= {int(s) for s in g.mon_step[ms:ms + mc] if 0 <= s < n_pad}
+        raw += len(need) * w
+    return table, raw
 
 
 def spot_vc(tag, out):
