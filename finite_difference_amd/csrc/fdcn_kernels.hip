@@ -188,15 +188,23 @@ __device__ __forceinline__ double bnd_eval(int form, double c0, double e0, doubl
 // zero (wave-uniform branches): c * exp(y) is c itself for c = +-0 and a
 // finite exp(y).  A call's lower and a put's upper Dirichlet value are such
 // terms (…pricer.py:381-391).  Used where the evaluation sits in the march
-// (kGen).
+// (kGen).  `skip` is the caller's uniform guarantee that every exp(e tau)
+// of the march is finite (e tau <= 700 at both ends of its tau range,
+// exp_finite_over): without it the exps are taken, so an overflowing
+// exponential keeps the reference's 0 * inf = NaN.
 __device__ __forceinline__ double bnd_eval_nz(int form, double c0, double e0, double c1,
-                                              double e1, double tau) {
-  const double t0 = c0 == 0.0 ? c0 : c0 * exp(e0 * tau);
+                                              double e1, double tau, bool skip) {
+  const double t0 = (skip && c0 == 0.0) ? c0 : c0 * exp(e0 * tau);
   if (form == 1) {
     const double p = t0 * c1;
-    return p == 0.0 ? p : p * exp(e1 * tau);
+    return (skip && p == 0.0) ? p : p * exp(e1 * tau);
   }
-  return t0 + (c1 == 0.0 ? c1 : c1 * exp(e1 * tau));
+  return t0 + ((skip && c1 == 0.0) ? c1 : c1 * exp(e1 * tau));
+}
+// exp(e0 tau) and exp(e1 tau) finite for tau in [ta, tb] (e tau is linear in tau)
+__host__ __device__ inline bool exp_finite_over(double e0, double e1, double ta, double tb) {
+  const double big = 700.0;
+  return e0 * ta <= big && e0 * tb <= big && e1 * ta <= big && e1 * tb <= big;
 }
 
 // Uniform per-phase (per theta) constants.
@@ -813,12 +821,14 @@ fdcn_march(KArgs A) {
       if constexpr (kGen) asm volatile("" : "+v"(x) : "v"(after));
       return x;
     };
-    auto ev = [](int f, double c0, double e0, double c1, double e1, double t)
+    auto ev = [](int f, double c0, double e0, double c1, double e1, double t, bool skip)
         __attribute__((always_inline)) {
-      return kGen ? bnd_eval_nz(f, c0, e0, c1, e1, t) : bnd_eval(f, c0, e0, c1, e1, t);
+      return kGen ? bnd_eval_nz(f, c0, e0, c1, e1, t, skip) : bnd_eval(f, c0, e0, c1, e1, t);
     };
-    const double lo = ev(q.lof, q.l0, q.l1, q.l2, q.l3, tau);
-    const double hi = ev(q.hif, q.h0, q.h1, q.h2, q.h3, seq(tau, lo));
+    const double t_b = q.t0 + 1.01 * (double)A.n_time * dt;
+    const double lo = ev(q.lof, q.l0, q.l1, q.l2, q.l3, tau, exp_finite_over(q.l1, q.l3, q.t0, t_b));
+    const double hi = ev(q.hif, q.h0, q.h1, q.h2, q.h3, seq(tau, lo),
+                         exp_finite_over(q.h1, q.h3, q.t0, t_b));
     raw = make_double2(lo, hi);
     if constexpr (IT) {
       const double lo_p = m == 0 ? v_lo0 : bnd_eval(q.lof, q.l0, q.l1, q.l2, q.l3, seq(tp, hi));
@@ -867,9 +877,7 @@ fdcn_march(KArgs A) {
     const double t_a = q.t0, t_b = q.t0 + 1.01 * (double)A.n_time * dt;
     auto side_const = [&](int f, double c0, double e0, double c1, double e1) {
       const bool zero = f == 1 ? (c0 == 0.0 || c1 == 0.0) : (c0 == 0.0 && c1 == 0.0);
-      const double big = 700.0;  // exp(e tau) finite over the march
-      return zero && isfinite(c0) && isfinite(c1) && e0 * t_a <= big && e0 * t_b <= big &&
-             e1 * t_a <= big && e1 * t_b <= big;
+      return zero && isfinite(c0) && isfinite(c1) && exp_finite_over(e0, e1, t_a, t_b);
     };
     if (side_const(q.lof, q.l0, q.l1, q.l2, q.l3)) tsel = 1;
     else if (side_const(q.hif, q.h0, q.h1, q.h2, q.h3)) tsel = 2;

@@ -361,7 +361,11 @@ __device__ __forceinline__ FactorClass factor_rows(const double* P, int n, int s
 // phases then agree on the pointwise form -- every Pricer2 and analytic-
 // overlay scenario whose middle row is not beside the barrier -- the
 // scenario is done, bitwise what the two-pass path below writes (it would
-// pick the same candidate: the first that classifies).  Otherwise (a phase
+// pick the same candidate: the first that classifies) -- up to the sign of
+// one zero: a row of the pair (i1, i1 + 1) that is not exceptional gets +0.0
+// here, where the two-pass path writes its pivot times a zero residual, -0.0
+// for a negative pivot; the march only adds these terms, so the
+// two differ at most in the sign of an exactly-zero result.  Otherwise (a phase
 // not classified at that alpha, the stencil form, or the diagnostics'
 // force_stencil) the general path classifies at all three candidates and
 // factors again.  diag read 1.0 times instead of ~1.33 per scenario.

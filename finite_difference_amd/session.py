@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import bisect
 import ctypes
+import threading
 import weakref
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
@@ -132,7 +133,16 @@ class Session:
     ``close()`` (and leaving the ``with`` block) destroys the session, unless
     arrays from ``host_buffer`` are still alive: the destroy then waits until
     the last of them is dropped (``close_pending``), so a view never outlives
-    the pinned memory it points into."""
+    the pinned memory it points into.
+
+    Threads: the session's device context (streams, events, pinned arena)
+    goes back to the idle pool of the thread that destroys it
+    (fdcn_session.hip), so the destroy runs on the thread that created the
+    session.  A deferred destroy whose last view is dropped on another thread
+    stays pending (``close_pending``) until the creating thread calls
+    ``close()`` again -- or, as a last resort, until the garbage collector
+    collects the session.  View finalizers do not run at interpreter exit
+    (atexit=False): a pending session is then left to process teardown."""
 
     def __init__(self):
         self._L = capi.lib()
@@ -143,6 +153,7 @@ class Session:
         self._h = h
         self._live_views = 0
         self._close_pending = False
+        self._owner = threading.get_ident()
 
     @property
     def closed(self) -> bool:
@@ -167,7 +178,10 @@ class Session:
 
     def _view_dropped(self) -> None:
         self._live_views -= 1
-        if self._live_views == 0 and self._close_pending:
+        # a deferred destroy runs on the creating thread only (class notes);
+        # dropped elsewhere, it stays pending for close() on that thread
+        if (self._live_views == 0 and self._close_pending and
+                threading.get_ident() == getattr(self, "_owner", None)):
             self._destroy()
 
     def __enter__(self) -> "Session":
@@ -197,7 +211,7 @@ class Session:
         capi._check(self._L.fdcn_session_host_buffer(self._h, 8 * m, ctypes.byref(p)))
         owner = _PinnedView(self, int(p.value), m)
         self._live_views += 1
-        weakref.finalize(owner, self._view_dropped)
+        weakref.finalize(owner, self._view_dropped).atexit = False
         return np.asarray(owner)[:int(n)]
 
     # -- steps ---------------------------------------------------------------

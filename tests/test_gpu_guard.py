@@ -19,6 +19,14 @@ each on a step count that fills whole 64-step chunks and on a ragged one
 (the last chunk partly past n_time), on the first and last scenario of the
 bench's own batch; the workspace ends at the last scenario's row, so a row
 offset or length past its end lands in the tail guard.
+
+Round 6: the same guard over EVERY compiled variant the
+planner can return -- each (waves, chunk, flavour) of kVariants, CN and IT:
+the multi-wave latency variants, the single-trade flavour, the paired
+flavour, and the variants with the correction table in the workspace --
+pinned with fdcn_force_variant on a grid that fills it, over 128 steps
+(two whole chunks) and 130 (a ragged third), three scenarios each (an odd
+batch: the paired flavour's last wave has no second scenario).
 """
 import os
 import sys
@@ -116,3 +124,104 @@ def test_march_stores_stay_in_their_buffers(workload, B, steps, instance, which,
     rel = np.max(np.abs(got - ref), axis=1) / scale
     print(f"[{workload} {instance} {g.n_nodes}x{nt} ws={ws_bytes}] max_rel_err={rel.max():.3e}")
     assert rel.max() <= TOL, rel
+
+
+# every compiled variant (fdcn_kernels.hip kVariants): (waves, npt, flavour,
+# table in the workspace); flavour 1 single-trade, 2 paired (CN only)
+ALL_VARIANTS = [(1, 2, 0), (1, 4, 0), (1, 8, 0), (1, 12, 0), (1, 16, 0), (1, 24, 0), (1, 32, 0),
+                (1, 40, 0), (1, 48, 0), (1, 64, 0), (2, 8, 0), (2, 16, 0), (2, 32, 0), (2, 40, 0),
+                (4, 8, 0), (4, 16, 0), (4, 24, 0), (4, 40, 0), (8, 8, 0), (8, 16, 0), (8, 40, 0),
+                (16, 8, 0), (16, 24, 0), (16, 40, 0), (1, 8, 1), (1, 16, 1), (1, 32, 1), (1, 8, 2)]
+ZG_VARIANTS = [(1, 64), (4, 40), (8, 40), (16, 40)]
+
+
+def _guarded_launch(g, k_cap, p):
+    dev = torch.device("cuda", 0)
+    P = torch.from_numpy(g.params).to(dev)
+    I = torch.from_numpy(g.iparams).to(dev)
+    V0 = torch.from_numpy(g.v_init).to(dev)
+    out = Guarded(g.B * g.n_nodes, dev)
+    ws_bytes = p["ws_bytes_per_scen"] * g.B
+    assert ws_bytes % 8 == 0
+    ws = Guarded(ws_bytes // 8, dev)
+    stream = torch.cuda.current_stream()
+    if g.it:
+        F = torch.from_numpy(g.payoff).to(dev)
+        capi.it_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, P.data_ptr(), I.data_ptr(),
+                          V0.data_ptr(), F.data_ptr(), out.ptr, k_cap, ws.ptr, ws_bytes,
+                          stream.cuda_stream)
+    else:
+        MS = torch.from_numpy(g.mon_step if len(g.mon_step) else np.zeros(1, np.int32)).to(dev)
+        MR = torch.from_numpy(g.mon_rebate if len(g.mon_rebate) else np.zeros(1)).to(dev)
+        capi.cn_batch_dev(g.B, g.n_nodes, g.n_time, g.n_ranna, P.data_ptr(), I.data_ptr(),
+                          V0.data_ptr(), len(g.mon_step), MS.data_ptr(), MR.data_ptr(), out.ptr,
+                          k_cap, ws.ptr, ws_bytes, stream.cuda_stream)
+    torch.cuda.synchronize()
+    return out, ws
+
+
+def _check_guarded(g, out, ws, label, tol):
+    assert out.guards_intact(), f"{label}: a store left v_out"
+    assert ws.guards_intact(), f"{label}: a store left the workspace"
+    got = out.values().reshape(g.B, g.n_nodes)
+    ref = _oracle(g)
+    scale = np.maximum(1.0, np.max(np.abs(ref), axis=1))
+    rel = np.max(np.abs(got - ref), axis=1) / scale
+    print(f"[{label}] max_rel_err={rel.max():.3e}")
+    assert rel.max() <= tol, rel
+
+
+@pytest.mark.parametrize("n_time", [128, 130], ids=["full_chunks", "ragged"])
+@pytest.mark.parametrize("it", [False, True], ids=["cn", "it"])
+@pytest.mark.parametrize("w,npt,fl", ALL_VARIANTS, ids=[f"w{w}n{n}f{f}" for w, n, f in ALL_VARIANTS])
+def test_every_variant_stores_stay_in_their_buffers(w, npt, fl, it, n_time, force_variant):
+    if it and fl == 2:
+        pytest.skip("the paired flavour is compiled for the CN march only")
+    from finite_difference_amd.engine import pack
+    from plan_factory import random_solve
+    force_variant(w, npt, fl)
+    n_nodes = (32 if fl == 2 else 64 * w) * npt - 3 + 2
+    # (few steps on a 40k-node grid: |fm| near 1 can need the correction
+    # table in the workspace -- the variant's ZG twin, also compiled -- or
+    # more LDS than the variant has: the first seeded batch that the pinned
+    # variant (or its twin) takes; checked on the host by the planner)
+    zg = 2 * fl if fl < 2 else 4
+    want = (f"fdcn_march<{int(it)},{w},{npt},{zg}>", f"fdcn_march<{int(it)},{w},{npt},{zg | 1}>")
+    for seed in range(8):
+        rng = np.random.default_rng(9000 + 31 * w + npt + 7 * fl + int(it) + n_time + 1000 * seed)
+        solves = [random_solve(rng, n_nodes, n_time, 2, it=it, drop_top=(i == 1))
+                  for i in range(3)]
+        for i, sv in enumerate(solves):
+            sv.tau_accumulate = i == 2
+        g = pack(solves, list(range(3)))
+        k_cap = capi.sm_extent(g.n_nodes, g.n_time, g.n_ranna, g.params)
+        name = capi.variant_name(g.n_nodes, it, k_cap, B=g.B)
+        if name in want:
+            break
+    assert name in want, name
+    p = capi.plan(g.n_nodes, it, k_cap, n_time=n_time, B=g.B)
+    out, ws = _guarded_launch(g, k_cap, p)
+    _check_guarded(g, out, ws, f"{name} n={n_nodes} m={n_time}",
+                   TOL * max(1.0, n_nodes / 2048))
+
+
+@pytest.mark.parametrize("it", [False, True], ids=["cn", "it"])
+@pytest.mark.parametrize("w,npt", ZG_VARIANTS, ids=[f"w{w}n{n}" for w, n in ZG_VARIANTS])
+def test_workspace_table_variants_stores_stay_in_their_buffers(w, npt, it, force_variant):
+    """The ZG variants (Sherman-Morrison table in the workspace, after the
+    boundary row): |fm| -> 1 on a grid that fills the variant, so the
+    correction extent needs more LDS than a CU has."""
+    from finite_difference_amd.engine import pack
+    from plan_factory import random_solve
+    force_variant(w, npt, 0)
+    n_nodes, n_time = 64 * w * npt - 3 + 2, 3
+    rng = np.random.default_rng(77 + w + int(it))
+    solves = [random_solve(rng, n_nodes, n_time, 2, it=it) for _ in range(3)]
+    g = pack(solves, list(range(3)))
+    k_cap = capi.sm_extent(g.n_nodes, g.n_time, g.n_ranna, g.params)
+    name = capi.variant_name(g.n_nodes, it, k_cap, B=g.B)
+    if name != f"fdcn_march<{int(it)},{w},{npt},1>":
+        pytest.skip(f"{name}: this grid's correction extent ({k_cap}) fits LDS")
+    p = capi.plan(g.n_nodes, it, k_cap, n_time=n_time, B=g.B)
+    out, ws = _guarded_launch(g, k_cap, p)
+    _check_guarded(g, out, ws, f"{name} n={n_nodes} k_cap={k_cap}", TOL * n_nodes / 2048)

@@ -101,3 +101,36 @@ def test_views_keep_the_session_object_alive(fake):
     del a, owner
     gc.collect()
     assert fake.destroyed == 1
+
+
+def test_last_view_dropped_on_another_thread_leaves_destroy_pending(fake):
+    """the session's device context goes back to the destroying
+    thread's pool, so a deferred destroy runs on the creating thread only.
+    The last view dropped on a worker thread leaves the session pending; the
+    creating thread's next close() destroys it."""
+    import threading
+    S = sess.Session()
+    box = [S.host_buffer(8)]
+    S.close()
+    assert S.close_pending and fake.destroyed == 0
+
+    def drop():
+        box.pop()
+        gc.collect()
+    t = threading.Thread(target=drop)
+    t.start()
+    t.join()
+    assert not box
+    gc.collect()
+    assert fake.destroyed == 0 and S.close_pending and not S.closed
+    S.close()  # the creating thread, no view left
+    assert fake.destroyed == 1 and S.closed
+
+
+def test_last_view_dropped_on_the_creating_thread_destroys(fake):
+    S = sess.Session()
+    a = S.host_buffer(8)
+    S.close()
+    del a
+    gc.collect()
+    assert fake.destroyed == 1 and S.closed

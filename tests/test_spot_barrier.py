@@ -429,3 +429,40 @@ def test_factor_scan_matches_serial_sweep_on_non_dominant_rows(alpha, spread):
                 assert err <= 1e-10, (stencil, k, err)
     finally:
         capi.vc_force_variant(0, 0, False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,npt,n", [(1, 16, 1025), (1, 10, 601), (4, 8, 2049)])
+def test_exceptional_rows_split_over_both_phases(w, npt, n):
+    """the one-pass path maps each phase's exceptional rows into
+    the pair (i1, i1 + 1) (csrc/fdcn_vc.hip, xi[ph][j] - i1).  Here the
+    Rannacher phase's only exceptional row is i1 + 1 and the CN phase's is
+    i1, so i1 comes from the other phase than the row it pairs with: the
+    scenario still classifies pointwise and both forms match the oracle."""
+    import dataclasses
+    from finite_difference_amd import capi
+    from finite_difference_amd.engine import pack_vc
+    base = _vanilla_solve(n, 60)
+    solves = []
+    for i1 in (1, npt - 1, npt, n // 2, n - 4):
+        D = base.diag.copy()
+        D[0, 3, i1 + 1] *= 1.001  # Rannacher phase: row i1 + 1
+        D[0, 5, i1 + 1] *= 0.999
+        D[1, 3, i1] *= 1.001      # Crank-Nicolson phase: row i1
+        D[1, 5, i1] *= 0.999
+        solves.append(dataclasses.replace(
+            base, diag=D, ko_lo=n // 4, ko_hi=3 * n // 4,
+            mon_steps=list(range(5, base.n_time + 1, 5)),
+            mon_rebates=[0.5] * len(range(5, base.n_time + 1, 5))))
+    g = pack_vc(solves, list(range(len(solves))))
+    assert np.all(capi.vc_forms(g.n_nodes, g.n_time, g.n_ranna, g.diag) == 1)
+    ref = oracle_engine().run_vc(solves)
+    try:
+        for stencil in (False, True):
+            capi.vc_force_variant(w, npt, stencil)
+            got = Engine().run_vc(solves)
+            for k, (a, b) in enumerate(zip(got, ref)):
+                err = float(np.max(np.abs(a - b))) / max(1.0, float(np.max(np.abs(b))))
+                assert err <= 1e-10, (stencil, k, err)
+    finally:
+        capi.vc_force_variant(0, 0, False)

@@ -9,6 +9,13 @@
 #                                                    (tools/build_ab.sh; WT = the in-tree
 #                                                    library) on bench workloads, interleaved
 #                                                    twice -> gpurun_out/OUT/WL_TAG_REP.json
+#   bash tools/gpu.sh sweep OUT WL "TAG ..." "B ..." [bench args...]
+#                                                    the same A/B over batch sizes
+#   bash tools/gpu.sh variants OUT WL "W,NPT[,F] ..." [bench args...]
+#                                                    one line per forced kernel variant
+#                                                    (bench.py --force-variant)
+#   bash tools/gpu.sh pmc-ab OUT "TAG ..." "WL ..."  SQ instruction / wait counters of each
+#                                                    build (one rocprofv3 --pmc pass each)
 #   bash tools/gpu.sh prof TAG WL [bench args...]    rocprofv3 --kernel-trace --stats of one
 #                                                    bench command -> gpurun_out/TAG/prof_WL
 #   bash tools/gpu.sh final TAG                      the end-of-round session (tools/gpu_final.sh)
@@ -45,6 +52,37 @@ case "$CMD" in
             exit $rc
           fi
         done
+      done
+    done ;;
+  sweep)
+    OUT=$1; WL=$2; TAGS=$3; BS=$4; shift 4
+    mkdir -p gpurun_out/$OUT
+    for B in $BS; do
+      for t in $TAGS; do
+        lib=""; [ "$t" != WT ] && lib="--lib ab/$t/libfdcn.so"
+        timeout -k 10 200 python bench.py $lib --workload $WL --batch $B --no-cpu-baseline "$@" \
+            > gpurun_out/$OUT/${t}_b$B.json 2>> gpurun_out/$OUT/ab.err || exit $?
+      done
+    done ;;
+  variants)
+    OUT=$1; WL=$2; VARS=$3; shift 3
+    mkdir -p gpurun_out/$OUT
+    for v in $VARS; do
+      timeout -k 10 200 python bench.py --force-variant "$v" --workload $WL --no-cpu-baseline "$@" \
+          > gpurun_out/$OUT/${WL}_${v//,/_}.json 2>> gpurun_out/$OUT/ab.err || exit $?
+    done ;;
+  pmc-ab)
+    OUT=$1; TAGS=$2; WLS=$3
+    for wl in $WLS; do
+      for t in $TAGS; do
+        O=gpurun_out/$OUT/${wl}_${t}
+        mkdir -p "$O"
+        lib=""; [ "$t" != WT ] && lib="--lib ab/$t/libfdcn.so"
+        timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS \
+            SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_SMEM \
+            --output-format csv -d "$O" -o sq -- \
+            python3 bench.py $lib --workload "$wl" --steps 2 --warmup 1 --no-cpu-baseline \
+            > "$O/sq.log" 2>&1 || exit $?
       done
     done ;;
   prof)
