@@ -62,6 +62,8 @@ def expected(wl):
     rd = g.params.nbytes + g.iparams.nbytes + vec * (2 if is_it else 1)
     rd += len(g.mon_step) * 12
     bnd = g.B * waves * n_pad * 16
+    if not is_it and waves == 1 and plan["npt"] > 40:
+        bnd = 0  # the recovery form evaluates its boundary terms in the march (round 5)
     raw_wr = 0
     if not is_it and waves == 1 and plan["npt"] <= 40:
         # the one-scenario split form (round 6): one-sided tables and the raw

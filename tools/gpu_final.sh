@@ -2,13 +2,18 @@
 # End-of-round measurement session on one GPU box: the -m gpu suite, every
 # bench workload's JSON line, rocprofv3 kernel-trace summaries of the default
 # bench, and the PMC passes bench.py reads (profiles/pmc_counters.json).
-# Usage: bash tools/gpu_final.sh TAG
+# Usage: bash tools/gpu_final.sh TAG [PART]   PART: all (default), lines (the
+# tests, smoke and every bench line) or profiles (rocprofv3 summaries, PMC
+# passes, the torchrun line) -- one gpurun call each when the whole session
+# would not fit one call's time limit
 set -o pipefail
 TAG=${1:-final}
+PART=${2:-all}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
+if [ "$PART" != profiles ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 \
     --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
 # the driver's smoke check (__graft_entry__.smoke, no build: the tree's .so)
@@ -30,6 +35,8 @@ timeout -k 10 300 python bench.py --workload spot_vc --n-space 600 --n-time 600 
 # config 4 with N = 2 ranks sharing this GPU over gloo (the N > 1 code path)
 FDCN_SHARE_DEVICE=1 timeout -k 10 300 python bench.py --gpus 2 --workload barrier --total 10000 \
     --backend gloo > $O/bench_barrier_total_2ranks_gloo.json 2> $O/bench_barrier_total_2ranks_gloo.err || exit $?
+fi
+[ "$PART" = lines ] && exit 0
 # the driver's bench command (--steps 20 --warmup 5): the summary's average
 # over 25 launches carries the one cold first launch at 1/25 weight
 for wl in american barrier double spot_vc; do
