@@ -893,26 +893,40 @@ fdcn_march(KArgs A) {
     // per chunk from a walk over the scenario's monitoring run (strictly
     // increasing entries, validated on the host)
     int mp = 0, mpe = 0;
-    bool edge_ko = false;
+    bool edge_ko = false, m_need_all = false;
     if constexpr (kTab1) {
       mp = Ui(I[FDCN_I_MON_START]);
       mpe = mp + Ui(I[FDCN_I_MON_COUNT]);
       edge_ko = Ui(I[FDCN_I_KO_LO]) >= 0 || n_nodes - 1 >= Ui(I[FDCN_I_KO_HI]);
+      m_need_all = edge_ko && mpe - mp >= A.n_time;  // a knock-out after every step
     }
     for (int c = 0; c < A.n_pad; c += kStride) {
       double2 raw;
       const double2 e = gen(c, raw);
       if (!valid) continue;  // a paired wave's missing scenario: no stores
       if constexpr (kTab1) {
-        unsigned long long need = 0ull;
-        while (edge_ko && mp < mpe) {
-          const int sm = Ui(A.mon_step[mp]);
-          if (sm >= c + kStride) break;
-          if (sm >= c) need |= 1ull << (sm - c);
-          ++mp;
+        // this chunk's monitor entries, 64 at a time: lane l loads entry
+        // mp + l; the run's entries below c + 64 are a prefix of them (sorted;
+        // an unsorted _dev run stops at its first larger entry, whose
+        // followers the march skips too), and each one in [c, c + 64) flags
+        // its step in the wave's boundary row of LDS (free until the march),
+        // which lane hl then reads back.  Monitoring on every step (config
+        // 5's window trade) needs every raw value: no walk.  (A scalar walk,
+        // one dependent load per entry, cost the 8 192-step single trade
+        // 1.3 ms.)
+        bool nd = m_need_all || (c + hl == A.n_time - 1);
+        if (!m_need_all && edge_ko && mp < mpe) {
+          int* flag = reinterpret_cast<int*>(bblk);
+          flag[lane] = 0;
+          const int sm = mp + lane < mpe ? A.mon_step[mp + lane] : 0x7fffffff;
+          const unsigned long long below =
+              (unsigned long long)__ballot(sm < c + kStride);
+          const int run_len = below == ~0ull ? 64 : __builtin_ctzll(~below);
+          if (lane < run_len && sm >= c) flag[sm - c] = 1;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          nd = nd || flag[hl] != 0;
+          mp += run_len;
         }
-        if (A.n_time - 1 >= c && A.n_time - 1 < c + kStride) need |= 1ull << (A.n_time - 1 - c);
-        const bool nd = (need >> hl) & 1ull;
         if (tsel) {
           bnd1[c + hl] = tsel == 1 ? e.y : e.x;
           if (nd) braw1[c + hl] = tsel == 1 ? raw.y : raw.x;
