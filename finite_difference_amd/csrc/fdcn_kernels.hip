@@ -386,6 +386,8 @@ constexpr int kKoRow = 32;
 // march they pushed the kernel's SGPRs into VGPR lanes: 260 registers, one
 // wave per SIMD)
 constexpr int kKoResRow = 4;
+// the one-sided boundary table (kTab1 in fdcn_march) from this batch size on
+constexpr int kTab1MinBatch = 256;
 typedef unsigned KoMask8 __attribute__((ext_vector_type(8)));  // 4 masks, s_load_dwordx8
 __device__ __forceinline__ unsigned long long ko_pair8(KoMask8 m, int j) {
   return ((unsigned long long)m[2 * j + 1] << 32) | m[2 * j];
@@ -865,7 +867,21 @@ fdcn_march(KArgs A) {
   // run: step s) and after the last step, so only those are stored, and
   // only for a scenario whose knock-out reaches an edge node.  Config 3's
   // table traffic: 0.96 GB -> ~0.33 GB per launch.
-  constexpr bool kTab1 = kTabSplit && !kPair;
+  // Throughput batches of 16-40-node chunks only (config 3's 1 024-node
+  // grids and the parity-mode barrier grids).  A single trade's march is
+  // latency-bound, and there the one-sided table's extra prologue work and
+  // live scalars cost ~4-6 % (trade_cnlog 0.41 -> 0.43 ms, trade_double 6.0
+  // -> 6.4 ms on one box, profiles/r06/tab1_gate/): the chunk lengths the
+  // single trades run on (8 and 12 nodes) do not compile it, and below
+  // kTab1MinBatch scenarios the kernel keeps the two-sided table and every
+  // raw value, as in round 5.
+#ifdef FDCN_NO_TAB1  // diagnostic builds only
+  constexpr bool kTab1 = false;
+#else
+  constexpr bool kTab1 = kTabSplit && !kPair && NPT >= 16;
+#endif
+  const bool tab1_on = kTab1 && A.B >= kTab1MinBatch;
+  (void)tab1_on;
   int tsel = 0;
   double rc_lo = 0.0, rc_hi = 0.0;  // the constant side's raw value
   (void)tsel;
@@ -875,7 +891,7 @@ fdcn_march(KArgs A) {
   double* braw1 = reinterpret_cast<double*>(bnd_raw);  // its raw values
   (void)bnd1;
   (void)braw1;
-  if constexpr (kTab1) {
+  if (tab1_on) {
     const Bnd q = bnd_params();
     const double t_a = q.t0, t_b = q.t0 + 1.01 * (double)A.n_time * dt;
     auto side_const = [&](int f, double c0, double e0, double c1, double e1) {
@@ -898,7 +914,8 @@ fdcn_march(KArgs A) {
       mp = Ui(I[FDCN_I_MON_START]);
       mpe = mp + Ui(I[FDCN_I_MON_COUNT]);
       edge_ko = Ui(I[FDCN_I_KO_LO]) >= 0 || n_nodes - 1 >= Ui(I[FDCN_I_KO_HI]);
-      m_need_all = edge_ko && mpe - mp >= A.n_time;  // a knock-out after every step
+      // a knock-out after every step, or a latency batch: every raw value
+      m_need_all = !tab1_on || (edge_ko && mpe - mp >= A.n_time);
     }
     for (int c = 0; c < A.n_pad; c += kStride) {
       double2 raw;

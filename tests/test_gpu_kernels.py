@@ -281,3 +281,28 @@ def test_rec_form_half_chunk_aggregates_vs_oracle(n_nodes, force_variant):
         solves.append(s)
     assert capi.plan(n_nodes, False, B=6)["npt"] == npt
     _compare(solves, f"rec half-chunk aggregates n={n_nodes}")
+
+
+@pytest.mark.parametrize("n_nodes,npt", [(1024, 16), (513, 8), (2134, 40)])
+def test_one_sided_table_batch_vs_oracle(n_nodes, npt):
+    """The one-sided boundary table (round 6; fdcn_march kTab1: chunks of 16
+    to 40 nodes, batches of kTab1MinBatch = 256 and more; the 513-node grid's
+    8-node chunks keep the two-sided table): calls (constant lower side), puts
+    (constant upper side, both Dirichlet forms), knock-outs that reach an
+    edge node or not, sparse and every-step monitoring, accumulated tau --
+    the raw values kept only for the steps after an edge knock-out, every
+    node against the oracle."""
+    rng = np.random.default_rng(777 + n_nodes)
+    B = 300
+    solves = []
+    for i in range(B):
+        s = random_solve(rng, n_nodes, 150, 2, it=False, drop_top=(i % 2 == 0))
+        s.tau_accumulate = i % 5 == 1
+        if i % 7 == 3:  # a knock-out on every step reaching node 0 / the last node
+            s.ko_lo, s.ko_hi = int(rng.integers(0, 40)), n_nodes - int(rng.integers(1, 40))
+            s.mon_steps = list(range(1, 151))
+            s.mon_rebates = [0.25] * 150
+        solves.append(s)
+    plan = capi.plan(n_nodes, False, B=B)
+    assert (plan["waves"], plan["npt"]) == (1, npt), plan
+    _compare(solves, f"one-sided table n={n_nodes} B={B}", tol=TOL * max(1.0, n_nodes / 2048))
