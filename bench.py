@@ -1140,6 +1140,8 @@ def bench_spot_vc(args):
     dev = torch.device("cuda", distributed.bind_device())
     n_space, n_time = args.n_space or 1024, args.n_time or 2000
     B = args.batch or DEFAULT_BATCH["spot_vc"]
+    if args.force_variant:  # A/B: W,NPT of fdcn_vc_march pinned
+        capi.vc_force_variant(*[int(x) for x in args.force_variant.split(",")[:2]])
     t_build = time.perf_counter()
     g = build_spot_vc(B, n_space, n_time)
     t_build = time.perf_counter() - t_build
