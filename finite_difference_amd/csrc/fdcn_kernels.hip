@@ -2548,21 +2548,22 @@ fdcn_march(KArgs A) {
                        "i"(16 * kKoRow + 36)
                      : "memory");
 #endif
-        // two statements of 32 slots (the front end counts a tied operand
-        // twice against the register file); exec is restored between them
-        // (the rebate moves in through the LDS unit, ds_read_b64, not the
-        // VALU: FDCN_KO_VMOV builds the v_mov_b64 form for A/B)
+        // statements of 16 slots at NPT 64 (the front end counts a tied
+        // operand twice against the register file; 16 measured faster than
+        // 32 or 8 there, see tools/gen_ko_res.py); exec is restored at the
+        // end of each.  The
+        // rebate moves in through the LDS unit (ds_read_b64), not the VALU;
+        // FDCN_KO_VMOV builds the v_mov_b64 form (statements of 32) for A/B
         const unsigned la = lds_addr(ko_rbs);
 #ifdef FDCN_KO_VMOV
-#define FDCN_KO_RES_FORM(N, B) FDCN_KO_RES_ASM_##N##_##B
+#define FDCN_KO_RES_CALL(N, B) FDCN_KO_RES_CALLF(FDCN_KO_RES_ASM_##N##_##B, FDCN_KO_RES_VOPS_##N##_##B)
 #else
-#define FDCN_KO_RES_FORM(N, B) FDCN_KO_RESL_ASM_##N##_##B
+#define FDCN_KO_RES_CALL(N, B) FDCN_KO_RES_CALLF(FDCN_KO_RESL_ASM_##N##_##B, FDCN_KO_RESL_VOPS_##N##_##B)
 #endif
-#define FDCN_KO_RES_CALL(N, B)                                                             \
-  asm volatile(FDCN_KO_RES_FORM(N, B)                                                      \
-               : FDCN_KO_RES_VOPS_##N##_##B, [q0] "+s"(q0), [q1] "+s"(q1), [cd] "=&s"(cd), \
-                 [mt] "=&s"(mt)                                                           \
-               : FDCN_KO_RES_INS(rebv, sv, q2, qd, c0, c1, kom_addr, la)                  \
+#define FDCN_KO_RES_CALLF(FORM, VOPS)                                              \
+  asm volatile(FORM                                                                \
+               : VOPS, [q0] "+s"(q0), [q1] "+s"(q1), [cd] "=&s"(cd), [mt] "=&s"(mt) \
+               : FDCN_KO_RES_INS(rebv, sv, q2, qd, c0, c1, kom_addr, la)          \
                : "scc", "memory")
 #if defined(FDCN_DIAG_KO) && FDCN_DIAG_KO == 2  // diagnostic: the loads only
         asm volatile("" ::"s"(q0), "s"(q1), "s"(q2), "s"(qd), "s"(c0), "s"(c1), "v"(rebv));
@@ -2573,13 +2574,17 @@ fdcn_march(KArgs A) {
         if constexpr (NPT == 64) {
           FDCN_KO_RES_CALL(64, 0);
           FDCN_KO_RES_CALL(64, 1);
-        } else {
+#ifndef FDCN_KO_VMOV
+          FDCN_KO_RES_CALL(64, 2);
+          FDCN_KO_RES_CALL(64, 3);
+#endif
+        } else {  // (48: statements of 32 slots, faster there)
           FDCN_KO_RES_CALL(48, 0);
           FDCN_KO_RES_CALL(48, 1);
         }
 #endif
 #undef FDCN_KO_RES_CALL
-#undef FDCN_KO_RES_FORM
+#undef FDCN_KO_RES_CALLF
       } else if constexpr (KoLoad<IT, W, NPT, ZG>::value) {
         // eight slots per block: each slot is one v_mov_b64 of the rebate
         // under an exec mask set on the scalar unit (s_and_b64 with the

@@ -56,11 +56,18 @@ def leaves(gsz):
     return out
 
 
-def gen_block(npt, blk, mode):
-    """Groups 4 blk .. 4 blk + 3 of a chunk of NPT slots (slots 32 blk ..
-    32 blk + 31): one asm statement.  Two statements per projection because
-    the front end counts a tied "+v" operand twice against the 256-VGPR file
-    (64 doubles in place would ask for 256 + 256).
+def gen_block(npt, blk, mode, gpb):
+    """Groups gpb blk .. gpb blk + gpb - 1 of a chunk of NPT slots (slots
+    8 gpb blk .. 8 gpb (blk + 1) - 1): one asm statement.  Several statements
+    per projection because the front end counts a tied "+v" operand twice
+    against the 256-VGPR file (64 doubles in place would ask for 256 + 256).
+    The v_mov_b64 form (A/B only) runs in statements of 32 slots (gpb 4), the
+    product's LDS form at NPT 64 in statements of 16 (gpb 2): config 5
+    13.05-13.12 ms with 32-slot statements, 12.30-12.34 with 16, 12.94-12.99
+    with 8, 13.50-13.55 with the first of two 32-slot statements left
+    undrained, all bitwise equal (profiles/r06/config5_ko/r06j_1drain,
+    r06k_gpb, r06l_g16).  At NPT 48 statements of 16 measured 0.6 % slower
+    (11.17-11.20 against 11.10 ms on a 3 073-node grid): it keeps 32.
 
     mode "v": each slot's rebate is a v_mov_b64 (VALU).  mode "l": an
     exec-masked ds_read_b64 of the rebate from one LDS slot ([la]), which
@@ -70,7 +77,7 @@ def gen_block(npt, blk, mode):
     compiler."""
     mov = ("v_mov_b64 %[v{}], %[rb]" if mode == "v" else "ds_read_b64 %[v{}], %[la]").format
     ng = npt // 8
-    groups = range(4 * blk, min(4 * blk + 4, ng))
+    groups = range(gpb * blk, min(gpb * blk + gpb, ng))
     main, special = [], []
     for g in groups:
         gsz = 7 if g == ng - 1 else 8
@@ -135,15 +142,18 @@ def gen_block(npt, blk, mode):
     tail = ["s_waitcnt lgkmcnt(0)"] if mode == "l" else []
     lines = head + main + special + ["99:"] + tail
     body = "".join(f'  "{l}\\n\\t" \\\n' for l in lines)
-    lo_slot, hi_slot = 32 * blk, min(32 * blk + 32, npt)
+    lo_slot, hi_slot = 8 * gpb * blk, min(8 * gpb * (blk + 1), npt)
     ops = ", ".join(f'[v{i}] "+v"(V[{i}])' for i in range(lo_slot, hi_slot))
     tag = "" if mode == "v" else "L"
     return (f"#define FDCN_KO_RES{tag}_ASM_{npt}_{blk} \\\n{body}  \"\"\n"
-            + (f"#define FDCN_KO_RES_VOPS_{npt}_{blk} {ops}\n" if mode == "v" else ""))
+            f"#define FDCN_KO_RES{tag}_VOPS_{npt}_{blk} {ops}\n")
 
 
 def gen(npt):
-    return "".join(gen_block(npt, b, m) for m in ("v", "l") for b in range((npt + 31) // 32))
+    ng = npt // 8
+    lg = 2 if npt == 64 else 4  # groups per statement of the LDS form
+    return ("".join(gen_block(npt, b, "v", 4) for b in range((ng + 3) // 4))
+            + "".join(gen_block(npt, b, "l", lg) for b in range((ng + lg - 1) // lg)))
 
 
 def render():
