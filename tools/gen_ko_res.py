@@ -64,9 +64,9 @@ def gen_block(npt, blk, mode, gpb):
     The v_mov_b64 form (A/B only) runs in statements of 32 slots (gpb 4), the
     product's LDS form at NPT 64 in statements of 16 (gpb 2): config 5
     13.05-13.12 ms with 32-slot statements, 12.30-12.34 with 16, 12.94-12.99
-    with 8, 13.50-13.55 with the first of two 32-slot statements left
-    undrained, all bitwise equal (profiles/r06/config5_ko/r06j_1drain,
-    r06k_gpb, r06l_g16).  At NPT 48 statements of 16 measured 0.6 % slower
+    with 8, 13.25-13.29 with 24 (24 + 24 + 16), 13.50-13.55 with the first
+    of two 32-slot statements left undrained, all bitwise equal
+    (profiles/r06/config5_ko/r06j_1drain, r06k_gpb, r06l_g16, r06m_g24).  At NPT 48 statements of 16 measured 0.6 % slower
     (11.17-11.20 against 11.10 ms on a 3 073-node grid): it keeps 32.
 
     mode "v": each slot's rebate is a v_mov_b64 (VALU).  mode "l": an
