@@ -11,7 +11,10 @@ S=gpurun_out/$TAG; D=profiles/$DEST
 mkdir -p "$D/pmc"
 cp "$S"/bench_*.json "$D/"
 cp "$S/gpu_tests.log" "$D/gpu_tests.txt"
+cp "$S/smoke.log" "$D/smoke.txt"
 for wl in american barrier double spot_vc; do
+  # the line of the rocprofv3 process beside its kernel-trace summary
+  cp "$S/prof_$wl.json" "$D/rocprof_bench_$wl.json"
   cp "$S/prof_$wl/${wl}_kernel_stats.csv" "$D/kernel_stats_$wl.csv"
   for p in fetch grbm sq write; do
     cp "gpurun_out/${TAG}_pmc_$wl/$p/${p}_counter_collection.csv" "$D/pmc/${wl}_$p.csv"

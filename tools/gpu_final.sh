@@ -1,7 +1,9 @@
 #!/bin/bash
 # End-of-round measurement session on one GPU box: the -m gpu suite, every
-# bench workload's JSON line, rocprofv3 kernel-trace summaries of the default
-# bench, and the PMC passes bench.py reads (profiles/pmc_counters.json).
+# bench workload's JSON line, the throughput lines under rocprofv3
+# --kernel-trace --stats (line and summary from one process), config 5's
+# two-stream record, the PMC passes bench.py reads (profiles/pmc_counters.json,
+# via tools/collect_final.sh) and the torchrun line.
 # Usage: bash tools/gpu_final.sh TAG [PART]   PART: all (default), lines (the
 # tests, smoke and every bench line) or profiles (rocprofv3 summaries, PMC
 # passes, the torchrun line) -- one gpurun call each when the whole session
@@ -37,12 +39,16 @@ FDCN_SHARE_DEVICE=1 timeout -k 10 300 python bench.py --gpus 2 --workload barrie
     --backend gloo > $O/bench_barrier_total_2ranks_gloo.json 2> $O/bench_barrier_total_2ranks_gloo.err || exit $?
 fi
 [ "$PART" = lines ] && exit 0
-# the driver's bench command (--steps 20 --warmup 5): the summary's average
-# over 25 launches carries the one cold first launch at 1/25 weight
+# the default bench command of each throughput config under rocprofv3: the
+# line (with its CPU baselines and parity record) and the kernel-trace
+# summary come from the same process
 for wl in american barrier double spot_vc; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o $wl -- \
-      python3 bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_$wl.log 2>&1 || exit $?
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o $wl -- \
+      python3 bench.py --workload $wl > $O/prof_$wl.json 2> $O/prof_$wl.err || exit $?
 done
+# config 5's two-stream record (a serving loop; the line stays one launch)
+timeout -k 10 300 python bench.py --workload double --overlap-streams --no-cpu-baseline \
+    > $O/bench_double_overlap.json 2> $O/bench_double_overlap.err || exit $?
 bash tools/pmc_counters.sh ${TAG}_pmc american barrier double spot_vc || exit $?
 # the launcher path the driver's scaling run uses (one rank here: one GPU)
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
