@@ -42,7 +42,9 @@ def _blocks(npt, form=""):
     (form "": the v_mov_b64 form, "L": the ds_read_b64 form the kernel runs)."""
     text = _gen().render()
     out = []
-    for blk in range((npt + 31) // 32):
+    # statements of 32 slots, or of 16 (the LDS form at NPT 64, gen_ko_res.py)
+    nblk = (npt + 15) // 16 if (form == "L" and npt == 64) else (npt + 31) // 32
+    for blk in range(nblk):
         m = re.search(rf"#define FDCN_KO_RES{form}_ASM_{npt}_{blk} \\\n((?:  \".*\" \\\n)+)",
                       text)
         assert m, (npt, blk)
