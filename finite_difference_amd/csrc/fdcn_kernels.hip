@@ -55,9 +55,6 @@
 #include "../../include/fdcn_diag.h"
 #include "fdcn_shared.h"
 #include "fdcn_ko_res.h"
-#ifdef FDCN_KO_DIAG  // diagnostic builds only: an A/B variant of the projection
-#include "fdcn_ko_res_diag.h"
-#endif
 
 namespace {
 
