@@ -306,3 +306,25 @@ def test_one_sided_table_batch_vs_oracle(n_nodes, npt):
     plan = capi.plan(n_nodes, False, B=B)
     assert (plan["waves"], plan["npt"]) == (1, npt), plan
     _compare(solves, f"one-sided table n={n_nodes} B={B}", tol=TOL * max(1.0, n_nodes / 2048))
+
+
+@pytest.mark.parametrize("n_nodes,B,n_ranna,variant", [
+    (2049, 2048, 2, "fdcn_march<1,1,32,0>"),   # config 2's instance
+    (1500, 300, 2, "fdcn_march<1,1,24,0>"),
+    (1500, 300, 0, "fdcn_march<1,1,24,0>")], ids=["config2", "npt24", "npt24_no_rannacher"])
+def test_it_throughput_batch_vs_oracle(n_nodes, B, n_ranna, variant):
+    """The IT throughput variants on throughput-sized batches (the planner's
+    own choice at these B, asserted): puts (both lower-boundary forms) and
+    calls, accumulated tau on a fifth of the solves, a non-zero tau0 on a
+    third, every node against the oracle over three 64-step blocks.  (Round 6
+    ran a one-sided-table build of these variants through it, measured and
+    not kept: profiles/r06/config2_tab1/.)"""
+    assert capi.variant_name(n_nodes, True, B=B) == variant
+    rng = np.random.default_rng(2049 + n_nodes + B + n_ranna)
+    solves = []
+    for i in range(B):
+        s = random_solve(rng, n_nodes, 150, n_ranna, it=True)
+        s.tau_accumulate = i % 5 == 1
+        s.tau0 = 0.0 if i % 3 else 0.021
+        solves.append(s)
+    _compare(solves, f"it one-sided table n={n_nodes} B={B} r={n_ranna}")
