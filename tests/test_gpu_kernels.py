@@ -327,4 +327,4 @@ def test_it_throughput_batch_vs_oracle(n_nodes, B, n_ranna, variant):
         s.tau_accumulate = i % 5 == 1
         s.tau0 = 0.0 if i % 3 else 0.021
         solves.append(s)
-    _compare(solves, f"it one-sided table n={n_nodes} B={B} r={n_ranna}")
+    _compare(solves, f"it throughput batch n={n_nodes} B={B} r={n_ranna}")
