@@ -2530,28 +2530,41 @@ fdcn_march(KArgs A) {
         const unsigned long long sv = __builtin_amdgcn_read_exec();
         unsigned long long q0, q1, q2, qd, mt;
         unsigned c0, c1, cd;
+        const unsigned la = lds_addr(ko_rbs);
+#ifdef FDCN_KO_VMOV
+#define FDCN_KO_RB_WRITE ""
+#else
+        // the LDS form's rebate word, written by lane 0 while the mask loads
+        // are in flight (the statements below read it back into the slots)
+#define FDCN_KO_RB_WRITE \
+  "s_mov_b64 %6, exec\n\ts_mov_b64 exec, 1\n\tds_write_b64 %14, %15\n\ts_mov_b64 exec, %6\n\t"
+#endif
+        unsigned long long sx;  // the saved exec of the write
 #if defined(FDCN_DIAG_KO) && FDCN_DIAG_KO == 1  // diagnostic: no loads (wrong masks)
         asm volatile("s_mov_b64 %0, 0\n\ts_mov_b64 %1, 0\n\ts_mov_b64 %2, 0\n\ts_mov_b64 %3, 0\n\t"
-                     "s_mov_b32 %4, 0\n\ts_mov_b32 %5, 0"
-                     : "=s"(q0), "=s"(q1), "=s"(q2), "=s"(qd), "=s"(c0), "=s"(c1));
+                     "s_mov_b32 %4, 0\n\ts_mov_b32 %5, 0\n\t" FDCN_KO_RB_WRITE
+                     : "=&s"(q0), "=&s"(q1), "=&s"(q2), "=&s"(qd), "=&s"(c0), "=&s"(c1), "=&s"(sx)
+                     : "s"(kom_addr), "i"(0), "i"(0), "i"(0), "i"(0), "i"(0), "i"(0), "v"(la),
+                       "v"(rebv)
+                     : "memory");
 #else
-        asm volatile("s_load_dwordx2 %0, %6, %7\n\ts_load_dwordx2 %1, %6, %8\n\t"
-                     "s_load_dwordx2 %2, %6, %9\n\ts_load_dwordx2 %3, %6, %10\n\t"
-                     "s_load_dword %4, %6, %11\n\ts_load_dword %5, %6, %12\n\t"
-                     "s_waitcnt lgkmcnt(0)"
-                     : "=s"(q0), "=s"(q1), "=s"(q2), "=s"(qd), "=s"(c0), "=s"(c1)
+        asm volatile("s_load_dwordx2 %0, %7, %8\n\ts_load_dwordx2 %1, %7, %9\n\t"
+                     "s_load_dwordx2 %2, %7, %10\n\ts_load_dwordx2 %3, %7, %11\n\t"
+                     "s_load_dword %4, %7, %12\n\ts_load_dword %5, %7, %13\n\t"
+                     FDCN_KO_RB_WRITE "s_waitcnt lgkmcnt(0)"
+                     : "=&s"(q0), "=&s"(q1), "=&s"(q2), "=&s"(qd), "=&s"(c0), "=&s"(c1), "=&s"(sx)
                      : "s"(kom_addr), "i"(16 * kKoRow), "i"(16 * kKoRow + 8),
                        "i"(16 * kKoRow + 16), "i"(16 * kKoRow + 24), "i"(16 * kKoRow + 32),
-                       "i"(16 * kKoRow + 36)
+                       "i"(16 * kKoRow + 36), "v"(la), "v"(rebv)
                      : "memory");
 #endif
+#undef FDCN_KO_RB_WRITE
         // statements of 16 slots at NPT 64 (the front end counts a tied
         // operand twice against the register file; 16 measured faster than
         // 32 or 8 there, see tools/gen_ko_res.py); exec is restored at the
         // end of each.  The
         // rebate moves in through the LDS unit (ds_read_b64), not the VALU;
         // FDCN_KO_VMOV builds the v_mov_b64 form (statements of 32) for A/B
-        const unsigned la = lds_addr(ko_rbs);
 #ifdef FDCN_KO_VMOV
 #define FDCN_KO_RES_CALL(N, B) FDCN_KO_RES_CALLF(FDCN_KO_RES_ASM_##N##_##B, FDCN_KO_RES_VOPS_##N##_##B)
 #else

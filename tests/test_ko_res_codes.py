@@ -229,6 +229,8 @@ def test_projection_moves_exactly_the_knocked_nodes(npt, form):
         assert nchg <= 2, (klo, khi)
         row = masks + [0] * (64 - npt)
         regs.update(rb=0, sv=(1 << 64) - 1, cd=0, mt=0, ka=0, la=0)
+        if form == "L":  # the kernel's mask-load statement wrote the rebate word
+            regs["_lds_written"] = True
         moved = [0] * npt
         for ins in blocks:
             assert run_block(ins, regs, row, moved) == (1 << 64) - 1  # exec restored
@@ -257,8 +259,25 @@ def test_row_fallback_path(form):
     masks = [int(x) for x in rng.integers(0, 1 << 62, npt)]
     regs = dict(q0=1, q1=2, q2=3, qd=masks[-1], c0=sum(63 << (6 * g) for g in range(5)),
                 c1=sum(63 << (6 * g) for g in range(3)), rb=0, sv=(1 << 64) - 1, cd=0, mt=0, ka=0,
-                la=0)
+                la=0, _lds_written=(form == "L"))  # (the kernel's mask-load statement)
     moved = [0] * npt
     for ins in blocks:
         run_block(ins, regs, masks, moved)
     assert moved == masks
+
+
+def test_lds_form_rebate_written_by_the_mask_load_statement():
+    """The LDS form's statements only read the rebate word; the kernel writes
+    it (lane 0, exec = 1, then exec restored) inside the statement that loads
+    the run masks, ahead of that statement's lgkmcnt(0) -- so the write has
+    landed before the first ds_read (LDS operations complete in order)."""
+    for npt in (64, 48):
+        for ins in _blocks(npt, "L"):
+            assert not any(i.startswith("ds_write") for i in ins), npt
+    src = open(os.path.join(ROOT, "finite_difference_amd", "csrc", "fdcn_kernels.hip")).read()
+    w = src.index("#define FDCN_KO_RB_WRITE \\")
+    body = src[w:src.index("#endif", w)]
+    assert "s_mov_b64 exec, 1" in body and "ds_write_b64 %14, %15" in body
+    assert "s_mov_b64 exec, %6" in body
+    load = src.index('FDCN_KO_RB_WRITE "s_waitcnt lgkmcnt(0)"')
+    assert load > w

@@ -71,7 +71,9 @@ def gen_block(npt, blk, mode, gpb):
 
     mode "v": each slot's rebate is a v_mov_b64 (VALU).  mode "l": an
     exec-masked ds_read_b64 of the rebate from one LDS slot ([la]), which
-    the first statement writes (lane 0) -- the LDS unit writes the VGPRs, so
+    the kernel writes (lane 0) in the statement that loads the run masks, so
+    the write's latency hides under theirs (12.40 -> 12.35 ms over four
+    interleaved pairs, r06aa/r06ab) -- the LDS unit writes the VGPRs, so
     the projection takes no VALU issue slot; each statement drains its reads
     (lgkmcnt(0)) before it ends, so its outputs are complete for the
     compiler."""
@@ -136,9 +138,7 @@ def gen_block(npt, blk, mode, gpb):
     if last:  # the chunk's last slot under its own mask
         main += ["s_and_b64 exec, %[qd], %[sv]", mov(npt - 1)]
     main += ["s_mov_b64 exec, %[sv]", "s_branch 99f"]
-    head = []
-    if mode == "l" and blk == 0:  # the rebate into the LDS slot, lane 0
-        head = ["s_mov_b64 exec, 1", "ds_write_b64 %[la], %[rb]"]
+    head = []  # (the LDS form's rebate word is written by the kernel's mask-load statement)
     tail = ["s_waitcnt lgkmcnt(0)"] if mode == "l" else []
     lines = head + main + special + ["99:"] + tail
     body = "".join(f'  "{l}\\n\\t" \\\n' for l in lines)
